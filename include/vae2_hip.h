@@ -1,0 +1,238 @@
+/*
+ * vae2_hip.h — C ABI of libvae2_hip.so, the MI355X (gfx950) kernels of the VAE²
+ * ELBO training step.
+ *
+ * The reference has no FFI: its hot path is Python calling ATen.
+ * Every entry point below replaces one ATen op class used by that path; the
+ * reference call site it stands in for is cited per function.
+ *
+ * Conventions
+ *   - Stateless launchers over CALLER-OWNED device buffers. The library never
+ *     allocates device memory; workspaces are sized by the *_size / *_rows queries.
+ *   - Activations are NHWC fp32 views described by vae2_act:
+ *        element (n, y, x, c) lives at ptr[((n*h + y)*w + x)*ps + c],  ps >= c.
+ *     A channel slice of a wider buffer is (ptr + c0, ps = width of the buffer).
+ *   - Conv weights keep the reference's nn.Conv2d layout [Cout][Cin][KH][KW]
+ *     (so state_dicts interchange); conv biases are [Cout].
+ *   - `stream` is a hipStream_t (PyTorch: torch.cuda.current_stream().cuda_stream).
+ *   - Return 0 on success, a hipError_t value on a launch error, or -22 (EINVAL)
+ *     for a bad argument; vae2_last_error() gives the message (thread-local).
+ */
+#ifndef VAE2_HIP_H
+#define VAE2_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vae2_act {
+  int64_t n, h, w, c;
+  int64_t ps; /* pixel stride, in elements */
+} vae2_act;
+
+#define VAE2_ABI_VERSION 1
+
+int vae2_abi_version(void);
+const char* vae2_last_error(void);
+
+/* ---------------------------------------------------------------- conv ---- */
+
+/* Rows of BN partial statistics that vae2_conv2d_fwd writes when stats != NULL
+ * (one row of `cout` sums and one of `cout` sums of squares per row).
+ * Workspace = 2 * rows * cout floats.                                         */
+int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout);
+
+/* y = conv2d(x, w, stride, pad) (+ bias) (+ beta*y), optional per-channel BN
+ * partial sums of the result in `stats` (layout [2][rows][cout]).
+ * Replaces nn.Conv2d.forward: conv3x3 enc_hrnet.py:27-30, Bottleneck 1x1
+ * :70-76, downsample :411-415, fuse :188-217, transitions :381-403, heads
+ * :323-370/:598-750, z head :1026-1039.                                       */
+int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* w,
+                    const float* bias, float* y, const vae2_act* yd, int k,
+                    int stride, int pad, float beta, float* stats,
+                    void* stream);
+
+/* Name of the kernel instantiation a vae2_conv2d_fwd launch with this output
+ * uses (e.g. "igemm_kernel<2, 4, 0>"), for matching timings with rocprof.     */
+int vae2_conv2d_fwd_kernel_name(const vae2_act* yd, int64_t cout, char* buf,
+                                int64_t len);
+
+/* dx = conv2d_transpose(dy, w) (+ beta*dx): gradient of vae2_conv2d_fwd w.r.t.
+ * its input (autograd's convolution_backward, input half).                    */
+int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* w,
+                         float* dx, const vae2_act* dxd, int k, int stride,
+                         int pad, float beta, void* stream);
+
+/* Workspace (floats) needed by vae2_conv2d_bwd_weight for this shape.         */
+int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd,
+                                       int k);
+
+/* dw (+)= sum_pixels dy (x) im2col(x); dbias (+)= sum_pixels dy if dbias.
+ * accumulate != 0 adds into dw/dbias (gradient buffers), else overwrites.
+ * (autograd's convolution_backward, weight half.)                            */
+int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
+                           const vae2_act* dyd, float* dw, float* dbias, int k,
+                           int stride, int pad, int accumulate, float* ws,
+                           int64_t ws_size, void* stream);
+
+/* ------------------------------------------------------------ batchnorm ---- */
+/* nn.BatchNorm2d(momentum=0.01, eps=1e-5) in train mode, enc_hrnet.py:22-23,
+ * (SyncBatchNorm when distributed, tools/train.py:216-218).                   */
+
+/* Rows of partials written by vae2_bn_stats / vae2_bn_relu_bwd_reduce.        */
+int64_t vae2_bn_partial_rows(const vae2_act* xd);
+
+/* Per-channel partial sums of x and x^2 -> partials [2][rows][c].             */
+int vae2_bn_stats(const float* x, const vae2_act* xd, float* partials,
+                  void* stream);
+
+/* partials [2][rows][c] (float) -> sums [2][c] (double, summed in fixed order).
+ * With accumulate != 0 the result is added to `sums`.                         */
+int vae2_bn_partials_reduce(const float* partials, int64_t rows, int64_t c,
+                            double* sums, int accumulate, void* stream);
+
+/* sums [2][c] = (sum x, sum x^2) over `count` values per channel (after an
+ * optional cross-rank all-reduce) -> save [4][c] = (mean, invstd, scale, shift)
+ * with scale = gamma*invstd, shift = beta - mean*scale; updates running stats
+ * (unbiased variance) and num_batches_tracked when those pointers are set.   */
+int vae2_bn_finalize(const double* sums, double count, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var,
+                     int64_t* num_batches_tracked, float momentum, float eps,
+                     int64_t c, float* save, void* stream);
+
+/* Eval mode: save [4][c] from running statistics.                              */
+int vae2_bn_eval_coeffs(const float* gamma, const float* beta,
+                        const float* running_mean, const float* running_var,
+                        float eps, int64_t c, float* save, void* stream);
+
+/* y = x*scale + shift (+ res) (then ReLU if relu).                             */
+int vae2_bn_apply(const float* x, const vae2_act* xd, const float* save,
+                  const float* res, const vae2_act* rd, float* y,
+                  const vae2_act* yd, int relu, void* stream);
+
+/* Backward reduce: g = dy * (y > 0 if relu); partials [2][rows][c] of
+ * (sum g, sum g*xhat), xhat = (x - mean)*invstd.                              */
+int vae2_bn_relu_bwd_reduce(const float* dy, const vae2_act* dyd,
+                            const float* y, const vae2_act* yd, const float* x,
+                            const vae2_act* xd, const float* save, int relu,
+                            float* partials, void* stream);
+
+/* dgamma (+)= sum g*xhat, dbeta (+)= sum g from local sums [2][c].            */
+int vae2_bn_bwd_param_grads(const double* sums, int64_t c, float* dgamma,
+                            float* dbeta, void* stream);
+
+/* dx = gamma*invstd*(g - sum_g/count - xhat*sum_gxhat/count);
+ * also dres = g when dres != NULL (residual branch of the block).             */
+int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
+                           const vae2_act* yd, const float* x,
+                           const vae2_act* xd, const float* save,
+                           const float* gamma, const double* sums, double count,
+                           int relu, float* dx, const vae2_act* dxd,
+                           float* dres, const vae2_act* dresd, void* stream);
+
+/* ----------------------------------------------- resample / fuse / concat ---- */
+
+/* y (+)= bilinear_upsample(x) to y's h,w, align_corners=False
+ * (F.interpolate/F.upsample mode='bilinear', enc_hrnet.py:242-245, :835-837,
+ * :1111-1113). beta: y = up(x) + beta*y.                                      */
+int vae2_upsample_bilinear_fwd(const float* x, const vae2_act* xd, float* y,
+                               const vae2_act* yd, float beta, void* stream);
+/* dx (+)= adjoint of the above applied to dy (beta: dx = adj + beta*dx).      */
+int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
+                               const vae2_act* dxd, float beta, void* stream);
+
+/* y = relu(sum_i up(x_i)) over n <= 4 terms; terms with smaller h,w than y
+ * are bilinearly upsampled (HighResolutionModule fuse, enc_hrnet.py:233-249). */
+int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
+                       float* y, const vae2_act* yd, void* stream);
+
+/* g = dy * (y > 0)  (ReLU backward, threshold_backward).                       */
+int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,
+                  const vae2_act* yd, float* g, const vae2_act* gd,
+                  void* stream);
+
+/* y = x (strided NHWC copy, e.g. into a channel slice for torch.cat).         */
+int vae2_copy_act(const float* x, const vae2_act* xd, float* y,
+                  const vae2_act* yd, float beta, void* stream);
+
+/* Code-map tiling (_gen_code_map, enc_hrnet.py:454-462): y[n,:,:,c] = v[n,c]
+ * for a per-clip vector v [n][vc] (vector stride vs).                          */
+int vae2_codemap_tile_fwd(const float* v, int64_t vs, float* y,
+                          const vae2_act* yd, void* stream);
+/* Workspace (floats) for the spatial reductions below.                          */
+int64_t vae2_spatial_ws_size(const vae2_act* xd);
+/* dv (+)= sum over h,w of dy[n,:,:,c].                                          */
+int vae2_codemap_tile_bwd(const float* dy, const vae2_act* dyd, float* dv,
+                          int64_t vs, int accumulate, float* ws, int64_t ws_size,
+                          void* stream);
+
+/* NCHW <-> NHWC layout conversion at the API boundary (clips are (B, 3L, H, W)
+ * tensors, cityscapes.py:311-326).                                             */
+int vae2_nchw_to_nhwc(const float* x, float* y, const vae2_act* yd,
+                      float beta, void* stream);
+int vae2_nhwc_to_nchw(const float* x, const vae2_act* xd, float* y,
+                      float beta, void* stream);
+
+/* AdaptiveAvgPool2d((1,1)) (enc_hrnet.py:1025): y[n][c] = mean_hw x.           */
+int vae2_global_avgpool_fwd(const float* x, const vae2_act* xd, float* y,
+                            const vae2_act* yd, float* ws, int64_t ws_size,
+                            void* stream);
+int vae2_global_avgpool_bwd(const float* dy, const vae2_act* dyd, float* dx,
+                            const vae2_act* dxd, float beta, void* stream);
+
+/* ------------------------------------------------------------- ELBO ---- */
+
+/* out[0] = sum |p - t| * scale  (L1Loss, criterion.py:61-69, scale = 1/B).
+ * ws: vae2_reduce_ws_size(n elements) floats.                                  */
+int64_t vae2_reduce_ws_size(int64_t n);
+int vae2_l1_fwd(const float* p, const vae2_act* pd, const float* t,
+                const vae2_act* td, float scale, float* ws, float* out,
+                void* stream);
+/* dp (+)= sign(p - t) * scale * gout[0] * (beta ? +prev : )                   */
+int vae2_l1_bwd(const float* p, const vae2_act* pd, const float* t,
+                const vae2_act* td, const float* gout, float scale, float* dp,
+                const vae2_act* dpd, float beta, void* stream);
+
+/* Reparameterisation + KL (utils.py:85-101, criterion.py:72-87).
+ * muvar: act with 2*zc channels (mu = [0,zc), logvar = [zc,2zc)); eps, z: acts
+ * with zc channels.  prior != 0: z = eps (prior_sampling).
+ * kl_out[0] (+)= scale * sum 0.5*(mu^2 + exp(lv) - lv - 1).                     */
+int vae2_reparam_kl_fwd(const float* muvar, const vae2_act* md,
+                        const float* eps, const vae2_act* ed, float* z,
+                        const vae2_act* zd, int prior, float scale,
+                        float* kl_out, int accumulate, float* ws, void* stream);
+/* dmuvar = dz-path + gkl[0]*scale*dKL;  dz may be NULL (no z gradient).        */
+int vae2_reparam_kl_bwd(const float* muvar, const vae2_act* md,
+                        const float* eps, const vae2_act* ed, const float* dz,
+                        const vae2_act* dzd, const float* gkl, float scale,
+                        float* dmuvar, const vae2_act* dmd, void* stream);
+
+/* total[0] = sum_i lambda_i * terms[i][0] (utils.py:150-152); n <= 8.          */
+int vae2_weighted_sum(int n, const float* const* terms, const float* lambdas,
+                      float* total, void* stream);
+
+/* flag[0] |= any(!isfinite(x)) (FullModel_encdec._anomoly_detection,
+ * utils.py:63-65). x is a dense array of n floats.                              */
+int vae2_nonfinite_check(const float* x, int64_t n, int32_t* flag,
+                         void* stream);
+
+/* ------------------------------------------------------------ optimizer ---- */
+
+/* torch.optim.Adam step (tools/train.py:251-261) over one flat fp32 buffer:
+ * m = b1*m + (1-b1)*g ; v = b2*v + (1-b2)*g^2 ;
+ * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps)   (+ L2 wd).      */
+int vae2_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
+                   float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t step, void* stream);
+
+/* dst = src * scale, for fp32 buffers (grad averaging after all-reduce).       */
+int vae2_scale(float* dst, const float* src, int64_t n, float scale,
+               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VAE2_HIP_H */

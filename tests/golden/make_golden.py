@@ -1,0 +1,201 @@
+"""Generate the golden vectors that pin oracle/ref_cpu.py to the reference.
+
+Runs ONLY in the build container, where /root/reference exists: it imports the
+reference's own modules (lib/models/enc_hrnet.py, lib/utils/utils.py,
+lib/core/criterion.py) read-only, with the two shims SURVEY.md App. C lists
+(numpy.int alias, an attribute-dict config instead of yacs), and writes data
+only (inputs, noise, outputs, loss terms, gradients, checksums) as .npz here.
+Nothing from the reference is copied.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz
+
+Cases
+  tiny_native   tiny HRNet, 32x32, B=2, L=3, Z=4, VAE_NATIVE:
+                inputs, eps/code, mu|logvar, z, x2t/x3t/xt predictions, loss terms,
+                every parameter gradient, 3 Adam steps (loss trajectory + param sums)
+  tiny_hdz      same with HD_Z (Z_DIM 3)
+  tiny_base     IS_BASELINE=True, VAE_NATIVE (decoders under no_grad, L1(x2t_hat, x3t))
+  w18           HRNet-W18-small-v2, 32x32, B=2, Z=10: outputs, losses, per-parameter
+                gradient norms, init checksums (weights regenerate from the seed)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference/lib"
+
+
+class AttrDict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+
+def stages(tiny):
+    if tiny:
+        return {"STAGE1": dict(NUM_MODULES=1, NUM_BRANCHES=1, BLOCK="BOTTLENECK", NUM_BLOCKS=[1],
+                               NUM_CHANNELS=[8], FUSE_METHOD="SUM"),
+                "STAGE2": dict(NUM_MODULES=1, NUM_BRANCHES=2, BLOCK="BASIC", NUM_BLOCKS=[1, 1],
+                               NUM_CHANNELS=[4, 8], FUSE_METHOD="SUM"),
+                "STAGE3": dict(NUM_MODULES=1, NUM_BRANCHES=3, BLOCK="BASIC",
+                               NUM_BLOCKS=[1, 1, 1], NUM_CHANNELS=[4, 8, 16], FUSE_METHOD="SUM"),
+                "STAGE4": dict(NUM_MODULES=1, NUM_BRANCHES=4, BLOCK="BASIC",
+                               NUM_BLOCKS=[1, 1, 1, 1], NUM_CHANNELS=[4, 8, 16, 32],
+                               FUSE_METHOD="SUM")}
+    return {"STAGE1": dict(NUM_MODULES=1, NUM_BRANCHES=1, BLOCK="BOTTLENECK", NUM_BLOCKS=[2],
+                           NUM_CHANNELS=[64], FUSE_METHOD="SUM"),
+            "STAGE2": dict(NUM_MODULES=1, NUM_BRANCHES=2, BLOCK="BASIC", NUM_BLOCKS=[2, 2],
+                           NUM_CHANNELS=[18, 36], FUSE_METHOD="SUM"),
+            "STAGE3": dict(NUM_MODULES=3, NUM_BRANCHES=3, BLOCK="BASIC", NUM_BLOCKS=[2, 2, 2],
+                           NUM_CHANNELS=[18, 36, 72], FUSE_METHOD="SUM"),
+            "STAGE4": dict(NUM_MODULES=2, NUM_BRANCHES=4, BLOCK="BASIC",
+                           NUM_BLOCKS=[2, 2, 2, 2], NUM_CHANNELS=[18, 36, 72, 144],
+                           FUSE_METHOD="SUM")}
+
+
+def make_cfg(tiny, hd=False, baseline=False, mode="VAE_NATIVE", z=None, L=3):
+    extra = AttrDict(IS_BASELINE=baseline, BASELINE_MODE=mode, Z_DIM=z or (4 if tiny else 10),
+                     HD_Z=hd, FINAL_CONV_KERNEL=1)
+    for k, v in stages(tiny).items():
+        extra[k] = AttrDict(v)
+    return AttrDict(MODEL=AttrDict(NAME="enc_hrnet", PRETRAINED="", EXTRA=extra),
+                    DATASET=AttrDict(NUM_CLASSES=3), TRAIN=AttrDict(CLIP_LENGTH=L, IMAGE_SIZE=[32, 32]))
+
+
+def checksums(sd):
+    names = sorted(sd)
+    s = np.array([float(sd[k].double().sum()) for k in names])
+    a = np.array([float(sd[k].double().abs().sum()) for k in names])
+    return names, s, a
+
+
+def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, W=32,
+             full_grads=False, adam_steps=0, z=None):
+    import torch
+    import models.enc_hrnet as eh
+    from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
+    from utils.utils import FullModel_encdec
+
+    cfg = make_cfg(tiny, hd, baseline, mode, z=z)
+    L = cfg.TRAIN.CLIP_LENGTH
+    zc = cfg.MODEL.EXTRA.Z_DIM
+    torch.manual_seed(0)
+    ed = eh.get_encdec_model(cfg)
+    ez = eh.get_encz_model(cfg)
+    ds = eh.get_D_sequence_model(cfg)
+    df = eh.get_D_frame_model(cfg)
+    init_ed = {k: v.clone() for k, v in ed.state_dict().items()}
+    init_ez = {k: v.clone() for k, v in ez.state_dict().items()}
+    fm = FullModel_encdec(ez, ed, ds, df, L1Loss(), KLLoss(), lsgan_adversarial_loss(),
+                          1.0, 0.1, 1.0, 0.0)
+    fm.train()
+    g = torch.Generator().manual_seed(1)
+    xt, x2t, x3t = [torch.randn(B, 3 * L, H, W, generator=g) for _ in range(3)]
+    out = {"xt": xt, "x2t": x2t, "x3t": x3t}
+
+    # capture every network's inputs/outputs with forward hooks
+    cap = {}
+    ed_fwd = ed.forward
+
+    def ed_hook(x, z=None, is_baseline=False):
+        cap["ed_in"] = x.detach().clone()
+        cap["ed_z"] = ([t.detach().clone() for t in z] if isinstance(z, list)
+                       else (z.detach().clone() if z is not None else None))
+        r = ed_fwd(x, z=z, is_baseline=is_baseline)
+        return r
+    ed.forward = ed_hook
+    ez.register_forward_hook(lambda m, i, o: cap.__setitem__(
+        "muvar", [t.detach().clone() for t in o] if isinstance(o, list) else o.detach().clone()))
+
+    torch.manual_seed(123)
+    losses, x1p, x2p, x3p = fm(xt, x2t, x3t, 1.0, is_baseline=baseline, baseline_mode=mode)
+    # replay the draws (eps then code; SURVEY.md App. C, verified bit-exact)
+    torch.manual_seed(123)
+    if mode != "DETERMINISTIC":
+        if hd:
+            eps = [torch.randn(B, zc, m.shape[2], m.shape[3]) for m in cap["muvar"]]
+        else:
+            eps = torch.randn(B, zc, 1, 1)
+    code = torch.randn(B, zc, 1, 1)
+    if mode != "DETERMINISTIC":
+        if hd:
+            for i, e in enumerate(eps):
+                out[f"eps{i}"] = e
+                out[f"muvar{i}"] = cap["muvar"][i]
+                out[f"z{i}"] = cap["ed_z"][i]
+        else:
+            out["eps"] = eps
+            out["muvar"] = cap["muvar"]
+            out["z"] = cap["ed_z"]
+    out["code"] = code
+    out["x1p"], out["x2p"], out["x3p"] = x1p.detach(), x2p.detach(), x3p.detach()
+    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
+    for n, v in zip(names, losses[:5]):
+        out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]) if torch.is_tensor(v) else v)
+    losses[0].backward()
+    params = [(n, p) for n, p in list(ez.named_parameters(prefix="encz")) +
+              list(ed.named_parameters(prefix="ed"))]
+    gnames = [n for n, p in params]
+    gnorm = np.array([float(p.grad.double().norm()) if p.grad is not None else 0.0
+                      for n, p in params])
+    out["grad_norms"] = torch.as_tensor(gnorm)
+    if full_grads:
+        for n, p in params:
+            if p.grad is not None:
+                out["grad/" + n] = p.grad.detach().clone()
+    # running statistics after one step
+    rs = {("encz." + k): v for k, v in ez.state_dict().items() if "running" in k}
+    rs.update({("ed." + k): v for k, v in ed.state_dict().items() if "running" in k})
+    rn, rsum, rabs = checksums(rs)
+    out["running_sum"] = torch.as_tensor(rsum)
+    out["running_abs"] = torch.as_tensor(rabs)
+    # init checksums (weights regenerate from torch.manual_seed(0))
+    _, s1, a1 = checksums(init_ed)
+    _, s2, a2 = checksums(init_ez)
+    out["init_ed_sum"], out["init_ed_abs"] = torch.as_tensor(s1), torch.as_tensor(a1)
+    out["init_ez_sum"], out["init_ez_abs"] = torch.as_tensor(s2), torch.as_tensor(a2)
+    if adam_steps:
+        ps = [p for n, p in list(ez.named_parameters()) + list(ed.named_parameters())]
+        opt = torch.optim.Adam([{"params": ps}], lr=1e-4)
+        traj = []
+        opt.step()  # step 1 uses the gradients computed above
+        for k in range(1, adam_steps):
+            opt.zero_grad()
+            torch.manual_seed(200 + k)
+            ls = fm(xt, x2t, x3t, 1.0, is_baseline=baseline, baseline_mode=mode)[0]
+            traj.append(float(ls[0]))
+            ls[0].backward()
+            opt.step()
+        out["adam_losses"] = torch.as_tensor(np.array(traj))
+        pn, psum, pabs = checksums({n: p.detach() for n, p in params})
+        out["adam_param_sum"] = torch.as_tensor(psum)
+        out["adam_param_abs"] = torch.as_tensor(pabs)
+    arrays = {k: v.detach().numpy().astype(np.float64 if v.dtype == torch.float64 else np.float32)
+              if torch.is_tensor(v) else np.asarray(v) for k, v in out.items()}
+    arrays["grad_names"] = np.array(gnames)
+    arrays["running_names"] = np.array(rn)
+    path = os.path.join(HERE, f"{tag}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def main():
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    np.int = int  # the reference uses the removed numpy alias (enc_hrnet.py:321,596,700)
+    import torch
+    torch.set_num_threads(8)
+    run_case("tiny_native", tiny=True, full_grads=True, adam_steps=3)
+    # Z_DIM 3: with 2*Z_DIM equal to a branch width the reference's HD_Z z-net has a
+    # None projection and fails (enc_hrnet.py:1018-1019, :1106)
+    run_case("tiny_hdz", tiny=True, hd=True, z=3)
+    run_case("tiny_base", tiny=True, baseline=True)
+    run_case("w18", tiny=False)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,238 @@
+"""Per-operator numerics of the HIP kernels (through vae2.ops) against plain
+PyTorch fp32 CPU references of the same ops, forward and backward."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from helpers import rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 2e-5  # fp32 MFMA (exact fma chains) vs oneDNN: reduction-order differences only
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+CONV_SHAPES = [
+    # N, H, W, Cin, Cout, k, stride, bias
+    (2, 16, 16, 18, 18, 3, 1, False),
+    (2, 17, 13, 9, 64, 3, 1, False),
+    (2, 16, 16, 36, 72, 3, 2, False),
+    (2, 15, 15, 18, 36, 3, 2, False),
+    (2, 8, 8, 270, 270, 1, 1, True),
+    (3, 1, 1, 270, 512, 1, 1, True),
+    (2, 12, 20, 256, 18, 3, 1, False),
+    (2, 16, 16, 64, 256, 1, 1, False),
+    (2, 9, 9, 5, 7, 1, 2, False),
+    (2, 8, 8, 154, 144, 3, 1, False),
+    (2, 32, 64, 64, 64, 3, 1, False),
+    (2, 8, 8, 270, 3, 1, 1, True),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_bwd(shape):
+    from vae2 import ops
+    torch.manual_seed(0)
+    n, h, w, cin, cout, k, s, bias = shape
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=bias)
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    y_ref = conv(x)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    # device copy; input given as a channel slice of a wider NHWC buffer
+    cg = nn.Conv2d(cin, cout, k, s, k // 2, bias=bias).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    big = torch.zeros(n, h, w, cin + 5, device=DEV)
+    big[..., 2:2 + cin] = nhwc(x.detach()).to(DEV)
+    xg = big[..., 2:2 + cin].requires_grad_(True)
+    yg = ops.conv(xg, cg)
+    yg.backward(nhwc(gy).to(DEV))
+    torch.cuda.synchronize()
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(nchw(xg.grad), x.grad) < TOL
+    assert rel(cg.weight.grad, conv.weight.grad) < TOL
+    if bias:
+        assert rel(cg.bias.grad, conv.bias.grad) < TOL
+
+
+@pytest.mark.parametrize("relu,res,stride", [(True, False, 1), (False, False, 2), (True, True, 1)])
+def test_conv_bn_train(relu, res, stride):
+    from vae2 import ops
+    torch.manual_seed(1)
+    n, h, w, cin, cout = 4, 12, 10, 18, 36
+    conv = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+    bn = nn.BatchNorm2d(cout, momentum=0.01)
+    nn.init.normal_(bn.weight, 1.0, 0.2)
+    nn.init.normal_(bn.bias, 0.0, 0.2)
+    conv_g, bn_g = conv.to(DEV), bn.to(DEV)
+    conv_c = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+    conv_c.load_state_dict({k: v.cpu() for k, v in conv_g.state_dict().items()})
+    bn_c = nn.BatchNorm2d(cout, momentum=0.01)
+    bn_c.load_state_dict({k: v.cpu() for k, v in bn_g.state_dict().items()})
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    oh = (h - 1) // stride + 1
+    ow = (w - 1) // stride + 1
+    r = torch.randn(n, cout, oh, ow, requires_grad=True) if res else None
+    y_ref = bn_c(conv_c(x))
+    if res:
+        y_ref = y_ref + r
+    if relu:
+        y_ref = F.relu(y_ref)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    xg = nhwc(x.detach()).to(DEV).requires_grad_(True)
+    rg = nhwc(r.detach()).to(DEV).requires_grad_(True) if res else None
+    yg = ops.conv_bn(xg, conv_g, bn_g, relu=relu, residual=rg)
+    yg.backward(nhwc(gy).to(DEV))
+    torch.cuda.synchronize()
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(nchw(xg.grad), x.grad) < 1e-4
+    assert rel(conv_g.weight.grad, conv_c.weight.grad) < 1e-4
+    assert rel(bn_g.weight.grad, bn_c.weight.grad) < 1e-4
+    assert rel(bn_g.bias.grad, bn_c.bias.grad) < 1e-5
+    if res:
+        assert rel(nchw(rg.grad), r.grad) < 1e-5
+    assert rel(bn_g.running_mean, bn_c.running_mean) < 1e-5
+    assert rel(bn_g.running_var, bn_c.running_var) < 1e-5
+    assert int(bn_g.num_batches_tracked) == int(bn_c.num_batches_tracked) == 1
+
+
+def test_conv_bn_eval():
+    from vae2 import ops
+    torch.manual_seed(2)
+    conv = nn.Conv2d(8, 16, 3, 1, 1, bias=False)
+    bn = nn.BatchNorm2d(16, momentum=0.01)
+    bn.running_mean.normal_()
+    bn.running_var.uniform_(0.5, 2.0)
+    conv.eval(), bn.eval()
+    x = torch.randn(2, 8, 9, 9)
+    y_ref = F.relu(bn(conv(x)))
+    cg, bg = nn.Conv2d(8, 16, 3, 1, 1, bias=False).to(DEV), nn.BatchNorm2d(16).to(DEV)
+    cg.load_state_dict(conv.state_dict()), bg.load_state_dict(bn.state_dict())
+    bg.eval()
+    with torch.no_grad():
+        yg = ops.conv_bn(nhwc(x).to(DEV), cg, bg, relu=True)
+    assert rel(nchw(yg), y_ref) < TOL
+
+
+@pytest.mark.parametrize("shapes", [[(16, 32), (8, 16), (4, 8), (2, 4)], [(9, 9), (5, 5), (3, 3)]])
+def test_up_cat(shapes):
+    from vae2 import ops
+    torch.manual_seed(3)
+    chans = [4, 8, 16, 32][:len(shapes)]
+    xs = [torch.randn(2, c, h, w, requires_grad=True) for c, (h, w) in zip(chans, shapes)]
+    hw = shapes[0]
+    y_ref = torch.cat([xs[0]] + [F.interpolate(x, size=list(hw), mode="bilinear",
+                                               align_corners=False) for x in xs[1:]], 1)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    xg = [nhwc(x.detach()).to(DEV).requires_grad_(True) for x in xs]
+    yg = ops.up_cat(xg)
+    yg.backward(nhwc(gy).to(DEV))
+    assert rel(nchw(yg), y_ref) < 1e-6
+    for a, b in zip(xg, xs):
+        assert rel(nchw(a.grad), b.grad) < 1e-5
+
+
+def test_fuse_sum_relu():
+    from vae2 import ops
+    torch.manual_seed(4)
+    hw = (16, 12)
+    terms = [torch.randn(2, 8, 16, 12, requires_grad=True),
+             torch.randn(2, 8, 16, 12, requires_grad=True),
+             torch.randn(2, 8, 8, 6, requires_grad=True),
+             torch.randn(2, 8, 2, 2, requires_grad=True)]
+    y = terms[0]
+    for tt in terms[1:]:
+        y = y + (tt if tt.shape[-2:] == hw else F.interpolate(tt, size=list(hw), mode="bilinear"))
+    y_ref = F.relu(y)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    tg = [nhwc(x.detach()).to(DEV).requires_grad_(True) for x in terms]
+    yg = ops.fuse_sum_relu(tg, hw)
+    yg.backward(nhwc(gy).to(DEV))
+    assert rel(nchw(yg), y_ref) < 1e-6
+    for a, b in zip(tg, terms):
+        assert rel(nchw(a.grad), b.grad) < 1e-5
+
+
+def test_cat_codemap_and_avgpool():
+    from vae2 import ops
+    torch.manual_seed(5)
+    code = torch.randn(3, 4, 1, 1)
+    z = torch.randn(3, 4, 1, 1, requires_grad=True)
+    x = torch.randn(3, 6, 5, 7, requires_grad=True)
+    y_ref = torch.cat([code.repeat(1, 1, 5, 7), z.repeat(1, 1, 5, 7), x], 1)
+    p_ref = F.adaptive_avg_pool2d(y_ref, 1)
+    gp = torch.randn_like(p_ref)
+    p_ref.backward(gp)
+    zg = nhwc(z.detach()).to(DEV).requires_grad_(True)
+    xg = nhwc(x.detach()).to(DEV).requires_grad_(True)
+    yg = ops.cat([nhwc(code).to(DEV), zg, xg], (5, 7), tiles=[True, True, False])
+    pg = ops.avgpool(yg)
+    pg.backward(nhwc(gp).to(DEV))
+    assert rel(nchw(yg), y_ref.detach()) == 0.0
+    assert rel(nchw(pg), p_ref) < 1e-6
+    assert rel(nchw(zg.grad), z.grad) < 1e-5
+    assert rel(nchw(xg.grad), x.grad) < 1e-6
+
+
+def test_l1_reparam_kl_weighted_sum():
+    from vae2 import ops
+    torch.manual_seed(6)
+    B, zc = 4, 10
+    p = torch.randn(B, 9, 6, 8, requires_grad=True)
+    tg = torch.randn(B, 9, 6, 8)
+    mv = torch.randn(B, 2 * zc, 1, 1, requires_grad=True)
+    eps = torch.randn(B, zc, 1, 1)
+    mu, lv = mv[:, :zc], mv[:, zc:]
+    z_ref = mu + torch.exp(torch.mul(lv, 0.5)) * eps
+    l1_ref = torch.sum(torch.abs(p - tg)) / B
+    kl_ref = torch.sum(0.5 * (mu ** 2 + torch.exp(lv) - lv - 1)) / B
+    gz = torch.randn_like(z_ref)
+    tot_ref = 1.0 * l1_ref + 0.5 * kl_ref + (z_ref * gz).sum()
+    tot_ref.backward()
+
+    pg = nhwc(p.detach()).to(DEV).requires_grad_(True)
+    mvg = nhwc(mv.detach()).to(DEV).requires_grad_(True)
+    zg, klg = ops.reparam_kl(mvg, nhwc(eps).to(DEV), scale=1.0 / B)
+    l1g = ops.l1(pg, nhwc(tg).to(DEV), 1.0 / B)
+    tot = ops.weighted_sum([l1g, klg], [1.0, 0.5])
+    (tot + (nchw(zg) * gz.to(DEV)).sum()).backward()
+    assert abs(float(l1g) - float(l1_ref)) <= 1e-6 * abs(float(l1_ref))
+    assert abs(float(klg) - float(kl_ref)) <= 1e-6 * abs(float(kl_ref))
+    assert rel(nchw(zg), z_ref) < 1e-6
+    assert rel(nchw(pg.grad), p.grad) < 1e-6
+    assert rel(nchw(mvg.grad), mv.grad) < 1e-6
+
+
+def test_fused_adam_matches_torch():
+    from vae2.optim import FusedAdam
+    torch.manual_seed(7)
+    m_ref = nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5))
+    m_gpu = nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5)).to(DEV)
+    m_gpu.load_state_dict(m_ref.state_dict())
+    opt_ref = torch.optim.Adam(m_ref.parameters(), lr=1e-3)
+    opt = FusedAdam([m_gpu], lr=1e-3)
+    for step in range(3):
+        grads = [torch.randn_like(p) for p in m_ref.parameters()]
+        for p, g in zip(m_ref.parameters(), grads):
+            p.grad = g.clone()
+        for p, g in zip(m_gpu.parameters(), grads):
+            p.main_grad.copy_(g)
+        opt_ref.step()
+        opt.step()
+    for a, b in zip(m_gpu.parameters(), m_ref.parameters()):
+        assert rel(a, b) < 1e-6
+    sd = opt.state_dict()
+    ref_sd = opt_ref.state_dict()
+    for k in ref_sd["state"]:
+        assert rel(sd["state"][k]["exp_avg"], ref_sd["state"][k]["exp_avg"]) < 1e-6

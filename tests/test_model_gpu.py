@@ -1,0 +1,148 @@
+"""Parity of the HIP ELBO step with the reference (golden vectors) and the oracle.
+
+Tolerances: the ELBO terms within 1e-5 relative; each
+network fed the reference's own inputs within 1e-4 relative (x2t_hat, mu|logvar,
+each decoder on the golden x2t_hat); end-to-end decoder frames within the
+reference's own fp32 spread (1e-3); gradients per tensor within 1e-3 rel-L2 on
+the tiny net.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import build, golden, make_cfg, max_rel, rel, t
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASES = {
+    "tiny_native": dict(arch="tiny"),
+    "tiny_hdz": dict(arch="tiny", hd=True, z=3),
+    "tiny_base": dict(arch="tiny", baseline=True),
+    "w18": dict(arch="w18"),
+}
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous().to(DEV)
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).detach().cpu()
+
+
+def hip_model(kw):
+    from vae2.model import FullModel_encdec
+    ed, ez = build(make_cfg(**kw))
+    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(DEV)
+    fm.train()
+    return fm
+
+
+def noise(g, hd):
+    eps = [t(g[f"eps{i}"]) for i in range(4)] if hd else t(g["eps"])
+    return eps, t(g["code"])
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_elbo_step_matches_reference(case):
+    kw = CASES[case]
+    g = golden(case)
+    fm = hip_model(kw)
+    fm.set_noise(*noise(g, kw.get("hd", False)))
+    losses, x1p, x2p, x3p = fm(t(g["xt"]).to(DEV), t(g["x2t"]).to(DEV), t(g["x3t"]).to(DEV), 1.0,
+                               is_baseline=kw.get("baseline", False))
+    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
+    for n, v in zip(names, losses[:5]):
+        ref = float(g["loss_" + n])
+        got = float(v.reshape(-1)[0]) if torch.is_tensor(v) else float(v)
+        assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-7, (n, got, ref)
+    assert max_rel(x2p, t(g["x2p"])) < 1e-4
+    assert rel(x3p, t(g["x3p"])) < 1e-3
+    assert rel(x1p, t(g["x1p"])) < 1e-3
+
+
+@pytest.mark.parametrize("case", ["tiny_native", "w18"])
+def test_each_network_on_golden_inputs(case):
+    """Per-network parity (1e-4): each net is fed the reference's own inputs."""
+    kw = CASES[case]
+    g = golden(case)
+    fm = hip_model(kw)
+    ed, ez = fm.encdec_model, fm.encz_model
+    with torch.no_grad():
+        mv = ez.run(nhwc(torch.cat([t(g["xt"]), t(g["x3t"])], 1)))
+        assert max_rel(nchw(mv), t(g["muvar"])) < 1e-4
+        z = nhwc(t(g["z"]))
+        x2p = ed.encode(nhwc(t(g["xt"])), z, nhwc(t(g["code"])))
+        assert max_rel(nchw(x2p), t(g["x2p"])) < 1e-4
+        gx2 = nhwc(t(g["x2p"]))
+        x3p = ed.decode("decf_", gx2, z)
+        x1p = ed.decode("decp_", gx2, z)
+        assert max_rel(nchw(x3p), t(g["x3p"])) < 1e-4
+        assert max_rel(nchw(x1p), t(g["x1p"])) < 1e-4
+
+
+def test_grads_running_stats_and_adam_match_reference():
+    from vae2.optim import FusedAdam
+    g = golden("tiny_native")
+    fm = hip_model(CASES["tiny_native"])
+    ed, ez = fm.encdec_model, fm.encz_model
+    opt = FusedAdam([ez, ed], lr=1e-4)
+    xt, x2t, x3t = (t(g[k]).to(DEV) for k in ("xt", "x2t", "x3t"))
+    fm.set_noise(*noise(g, False))
+    opt.zero_grad()
+    losses = fm(xt, x2t, x3t, 1.0)[0]
+    losses[0].backward()
+    params = list(ez.named_parameters(prefix="encz")) + list(ed.named_parameters(prefix="ed"))
+    ref_norms = g["grad_norms"]
+    floor = 1e-6 * ref_norms.max()
+    for (n, p), rn in zip(params, ref_norms):
+        key = "grad/" + n
+        if rn > floor:
+            assert rel(p.main_grad, t(g[key])) < 1e-3, n
+        else:  # analytically zero (conv bias in front of a BatchNorm)
+            assert float(p.main_grad.norm()) <= 1e-3 * float(ref_norms.max()), n
+    # running statistics after the step
+    rs = {("encz." + k): v for k, v in ez.state_dict().items() if "running" in k}
+    rs.update({("ed." + k): v for k, v in ed.state_dict().items() if "running" in k})
+    names = sorted(rs)
+    assert names == list(g["running_names"])
+    rsum = np.array([float(rs[k].double().sum()) for k in names])
+    np.testing.assert_allclose(rsum, g["running_sum"], rtol=1e-4, atol=1e-6)
+    # 3 Adam steps (lr 1e-4) vs the reference's torch.optim.Adam trajectory
+    opt.step()
+    traj = []
+    for k in range(1, 3):
+        opt.zero_grad()
+        torch.manual_seed(200 + k)
+        fm.set_noise(torch.randn(2, 4, 1, 1), torch.randn(2, 4, 1, 1))
+        ls = fm(xt, x2t, x3t, 1.0)[0]
+        traj.append(float(ls[0]))
+        ls[0].backward()
+        opt.step()
+    np.testing.assert_allclose(traj, g["adam_losses"], rtol=1e-5)
+    psum = np.array([float(p.detach().double().sum()) for _, p in sorted(params)])
+    np.testing.assert_allclose(psum, g["adam_param_sum"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("L,hw,B", [(2, (64, 64), 4), (3, (36, 20), 2)])
+def test_hip_matches_oracle_other_shapes(L, hw, B):
+    """Config ② geometry (64x64, 2 ctx + 4 pred -> L=2, B=4) and a ragged size."""
+    from oracle import ref_cpu
+    kw = dict(arch="w18", L=L, hw=hw)
+    cfg = make_cfg(**kw)
+    ed, ez = build(cfg)
+    ed_c, ez_c = copy.deepcopy(ed), copy.deepcopy(ez)
+    gen = torch.Generator().manual_seed(1)
+    xs = [torch.randn(B, 3 * L, *hw, generator=gen) for _ in range(3)]
+    eps = torch.randn(B, 10, 1, 1, generator=gen)
+    code = torch.randn(B, 10, 1, 1, generator=gen)
+    terms, preds, _ = ref_cpu.elbo(ez_c, ed_c, *xs, eps, code)
+    from vae2.model import FullModel_encdec
+    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(DEV)
+    fm.set_noise(eps, code)
+    losses, x1p, x2p, x3p = fm(*[x.to(DEV) for x in xs], 1.0)
+    ref = float(terms["loss_all"])
+    assert abs(float(losses[0]) - ref) <= 1e-5 * abs(ref)
+    assert max_rel(x2p, preds[1]) < 1e-4

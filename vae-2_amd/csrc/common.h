@@ -1,0 +1,84 @@
+// Shared helpers for the gfx950 kernels of libvae2_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <stdio.h>
+
+#include "../../include/vae2_hip.h"
+
+namespace vae2 {
+
+// ------------------------------------------------------------ errors ----
+void set_error(const std::string& msg);
+int fail(const char* fn, const std::string& msg);  // returns -22
+int check_launch(const char* fn);                   // hipGetLastError -> code
+
+#define VAE2_REQUIRE(cond, fn, msg)          \
+  do {                                       \
+    if (!(cond)) return ::vae2::fail(fn, msg); \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------- activations ----
+// Device-side copy of vae2_act with 32-bit-safe strides kept in 64-bit.
+struct Act {
+  int64_t n, h, w, c, ps;
+};
+
+inline Act to_act(const vae2_act* d) { return Act{d->n, d->h, d->w, d->c, d->ps}; }
+
+inline bool act_ok(const vae2_act* d) {
+  return d && d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && d->ps >= d->c;
+}
+
+inline int64_t act_pixels(const vae2_act* d) { return d->n * d->h * d->w; }
+inline int64_t act_elems(const vae2_act* d) { return d->n * d->h * d->w * d->c; }
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Division by a runtime constant via multiply-high (valid for n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+  FastDiv() : d(1), m(0), s(0) {}
+  explicit FastDiv(uint32_t div) : d(div) {
+    for (s = 0; s < 32; ++s)
+      if ((1u << s) >= d) break;
+    uint64_t one = 1;
+    m = (uint32_t)(((one << 32) * ((one << s) - d)) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (__umulhi(n, m) + n) >> s;
+  }
+};
+
+// Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
+int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
+                            float* dbias, int accumulate, void* stream);
+
+// Grid size for element-wise kernels: enough blocks to fill 256 CUs several
+// times over, each thread grid-striding.
+inline unsigned ew_blocks(int64_t n, int threads = 256, int64_t cap = 8192) {
+  int64_t b = ceil_div(n, threads);
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace vae2

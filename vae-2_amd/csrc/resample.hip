@@ -1,0 +1,501 @@
+// Bilinear resampling, multi-resolution fuse sums, code-map tiling, layout
+// conversion and global average pooling for NHWC fp32 activations.
+//
+//   F.interpolate / F.upsample(mode='bilinear', align_corners=False)
+//       enc_hrnet.py:242-245 (fuse), :835-837 / :893-895 / :951-953 (heads),
+//       :1111-1113 (z-net)                              -> upsample fwd / bwd
+//   HighResolutionModule fuse sum + ReLU :233-249      -> fuse_sum_relu
+//   _gen_code_map + torch.cat :454-462, :819-827       -> codemap tile fwd / bwd
+//   nn.AdaptiveAvgPool2d((1,1)) :1025                  -> global avgpool fwd / bwd
+#include "common.h"
+
+
+namespace vae2 {
+
+// ------------------------------------------------------------- errors ----
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(const char* fn, const std::string& msg) {
+  set_error(std::string(fn) + ": " + msg);
+  return -22;
+}
+
+int check_launch(const char* fn) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(fn) + ": " + hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+
+// ------------------------------------------------- bilinear helpers ----
+// PyTorch's area_pixel_compute_source_index for align_corners=False, in fp32.
+struct Lerp {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lerp lerp_index(int dst, int in_size, float scale) {
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  int i0 = (int)src;
+  if (i0 > in_size - 1) i0 = in_size - 1;
+  int ip = (i0 < in_size - 1) ? 1 : 0;
+  Lerp l;
+  l.i0 = i0;
+  l.i1 = i0 + ip;
+  l.l1 = src - (float)i0;
+  l.l0 = 1.f - l.l1;
+  return l;
+}
+
+__device__ __forceinline__ float bilinear_at(const float* __restrict__ x, const Act& xd,
+                                             int64_t n, int oy, int ox, int c, float sh,
+                                             float sw) {
+  Lerp ly = lerp_index(oy, (int)xd.h, sh);
+  Lerp lx = lerp_index(ox, (int)xd.w, sw);
+  const float* base = x + n * xd.h * xd.w * xd.ps + c;
+  float x00 = base[((int64_t)ly.i0 * xd.w + lx.i0) * xd.ps];
+  float x01 = base[((int64_t)ly.i0 * xd.w + lx.i1) * xd.ps];
+  float x10 = base[((int64_t)ly.i1 * xd.w + lx.i0) * xd.ps];
+  float x11 = base[((int64_t)ly.i1 * xd.w + lx.i1) * xd.ps];
+  return ly.l0 * (lx.l0 * x00 + lx.l1 * x01) + ly.l1 * (lx.l0 * x10 + lx.l1 * x11);
+}
+
+// Weight with which output coordinate `o` reads input coordinate `i`.
+__device__ __forceinline__ float lerp_weight(int o, int in_size, float scale, int i) {
+  Lerp l = lerp_index(o, in_size, scale);
+  float w = 0.f;
+  if (l.i0 == i) w += l.l0;
+  if (l.i1 == i) w += l.l1;
+  return w;
+}
+
+__global__ __launch_bounds__(256) void upsample_fwd_kernel(const float* __restrict__ x, Act xd,
+                                                           float* __restrict__ y, Act yd,
+                                                           float beta, FastDiv cdiv,
+                                                           FastDiv wdiv, FastDiv hdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  const float sh = (float)xd.h / (float)yd.h;
+  const float sw = (float)xd.w / (float)yd.w;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    uint32_t row = wdiv.div(p);
+    uint32_t ox = p - row * (uint32_t)yd.w;
+    uint32_t n = hdiv.div(row);
+    uint32_t oy = row - n * (uint32_t)yd.h;
+    float v = bilinear_at(x, xd, n, oy, ox, c, sh, sw);
+    float* dst = y + (int64_t)p * yd.ps + c;
+    *dst = (beta != 0.f) ? v + beta * *dst : v;
+  }
+}
+
+// Adjoint: dx[n,iy,ix,c] = sum_{oy,ox} wy(oy,iy) wx(ox,ix) dy[n,oy,ox,c].
+__global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restrict__ dy, Act dyd,
+                                                           float* __restrict__ dx, Act dxd,
+                                                           float beta, FastDiv cdiv,
+                                                           FastDiv wdiv, FastDiv hdiv) {
+  const uint32_t C = (uint32_t)dxd.c;
+  const uint32_t total = (uint32_t)(dxd.n * dxd.h * dxd.w) * C;
+  const float sh = (float)dxd.h / (float)dyd.h;
+  const float sw = (float)dxd.w / (float)dyd.w;
+  const int OH = (int)dyd.h, OW = (int)dyd.w;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    uint32_t row = wdiv.div(p);
+    int ix = (int)(p - row * (uint32_t)dxd.w);
+    uint32_t n = hdiv.div(row);
+    int iy = (int)(row - n * (uint32_t)dxd.h);
+    // candidate output ranges (exactly re-checked by lerp_weight)
+    int ylo = (int)floorf(((float)iy - 0.5f) / sh - 0.5f) - 1;
+    int yhi = (int)ceilf(((float)iy + 1.5f) / sh - 0.5f) + 1;
+    int xlo = (int)floorf(((float)ix - 0.5f) / sw - 0.5f) - 1;
+    int xhi = (int)ceilf(((float)ix + 1.5f) / sw - 0.5f) + 1;
+    if (ylo < 0) ylo = 0;
+    if (xlo < 0) xlo = 0;
+    if (yhi > OH - 1) yhi = OH - 1;
+    if (xhi > OW - 1) xhi = OW - 1;
+    // the last input row/col also collects every output beyond the range
+    if (iy == (int)dxd.h - 1) yhi = OH - 1;
+    if (ix == (int)dxd.w - 1) xhi = OW - 1;
+    const float* base = dy + (int64_t)n * OH * OW * dyd.ps + c;
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      float wy = lerp_weight(oy, (int)dxd.h, sh, iy);
+      if (wy == 0.f) continue;
+      float accx = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        float wx = lerp_weight(ox, (int)dxd.w, sw, ix);
+        if (wx == 0.f) continue;
+        accx += wx * base[((int64_t)oy * OW + ox) * dyd.ps];
+      }
+      acc += wy * accx;
+    }
+    float* dst = dx + (int64_t)p * dxd.ps + c;
+    *dst = (beta != 0.f) ? acc + beta * *dst : acc;
+  }
+}
+
+struct FuseTerms {
+  const float* x[4];
+  Act d[4];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* __restrict__ y,
+                                                            Act yd, FastDiv cdiv, FastDiv wdiv,
+                                                            FastDiv hdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    uint32_t row = wdiv.div(p);
+    uint32_t ox = p - row * (uint32_t)yd.w;
+    uint32_t n = hdiv.div(row);
+    uint32_t oy = row - n * (uint32_t)yd.h;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= t.n) break;
+      const Act& d = t.d[k];
+      float v;
+      if (d.h == yd.h && d.w == yd.w)
+        v = t.x[k][(int64_t)p * d.ps + c];
+      else
+        v = bilinear_at(t.x[k], d, n, oy, ox, c, (float)d.h / (float)yd.h,
+                        (float)d.w / (float)yd.w);
+      acc = (k == 0) ? v : acc + v;
+    }
+    y[(int64_t)p * yd.ps + c] = acc > 0.f ? acc : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy, Act dyd,
+                                                       const float* __restrict__ y, Act yd,
+                                                       float* __restrict__ g, Act gd,
+                                                       FastDiv cdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    float v = dy[(int64_t)p * dyd.ps + c];
+    g[(int64_t)p * gd.ps + c] = (y[(int64_t)p * yd.ps + c] > 0.f) ? v : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void copy_act_kernel(const float* __restrict__ x, Act xd,
+                                                       float* __restrict__ y, Act yd, float beta,
+                                                       FastDiv cdiv) {
+  const uint32_t C = (uint32_t)xd.c;
+  const uint32_t total = (uint32_t)(xd.n * xd.h * xd.w) * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    float v = x[(int64_t)p * xd.ps + c];
+    float* dst = y + (int64_t)p * yd.ps + c;
+    *dst = (beta != 0.f) ? v + beta * *dst : v;
+  }
+}
+
+// y[n,h,w,c] = scale * v[n*vs + c] + beta * y
+__global__ __launch_bounds__(256) void tile_kernel(const float* __restrict__ v, int64_t vs,
+                                                   float* __restrict__ y, Act yd, float scale,
+                                                   float beta, FastDiv cdiv, FastDiv hwdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    uint32_t n = hwdiv.div(p);
+    float val = scale * v[(int64_t)n * vs + c];
+    float* dst = y + (int64_t)p * yd.ps + c;
+    *dst = (beta != 0.f) ? val + beta * *dst : val;
+  }
+}
+
+// Spatial sums per (n, c): stage 1 partials over pixel chunks.
+__global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __restrict__ x,
+                                                               Act xd, int64_t ppb,
+                                                               float* __restrict__ part) {
+  __shared__ float red[256];
+  const int C = (int)xd.c;
+  const int64_t HW = xd.h * xd.w;
+  const int64_t n = blockIdx.y;
+  const int64_t p0 = blockIdx.x * ppb;
+  int64_t p1 = p0 + ppb;
+  if (p1 > HW) p1 = HW;
+  const float* base = x + n * HW * xd.ps;
+  float* out = part + (n * gridDim.x + blockIdx.x) * (int64_t)C;
+  const int tid = threadIdx.x;
+  if (C <= 256) {
+    const int R = 256 / C, S = R * C;
+    float s = 0.f;
+    if (tid < S) {
+      const int c = tid % C, rr = tid / C;
+      for (int64_t p = p0 + rr; p < p1; p += R) s += base[p * xd.ps + c];
+    }
+    red[tid] = s;
+    __syncthreads();
+    if (tid < C) {
+      float a = 0.f;
+      for (int i = 0; i < R; ++i) a += red[tid + i * C];
+      out[tid] = a;
+    }
+  } else {
+    for (int c = tid; c < C; c += 256) {
+      float s = 0.f;
+      for (int64_t p = p0; p < p1; ++p) s += base[p * xd.ps + c];
+      out[c] = s;
+    }
+  }
+}
+
+// stage 2: out[n*os + c] (+)= scale * sum_chunks part[n][chunk][c]
+__global__ void spatial_finish_kernel(const float* __restrict__ part, int64_t chunks, int64_t N,
+                                      int64_t C, float* out, int64_t os, float scale,
+                                      int accumulate) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  int64_t n = i / C, c = i - n * C;
+  float s = 0.f;
+  for (int64_t k = 0; k < chunks; ++k) s += part[(n * chunks + k) * C + c];
+  s *= scale;
+  float* dst = out + n * os + c;
+  *dst = accumulate ? *dst + s : s;
+}
+
+static int64_t spatial_chunks(const vae2_act* xd, int64_t* ppb_out) {
+  int64_t HW = xd->h * xd->w;
+  int64_t chunks = ceil_div(HW, 512);
+  if (chunks > 64) chunks = 64;
+  int64_t ppb = ceil_div(HW, chunks);
+  if (ppb_out) *ppb_out = ppb;
+  return ceil_div(HW, ppb);
+}
+
+static int spatial_sum(const float* x, const vae2_act* xd, float* out, int64_t os,
+                       float scale, int accumulate, float* part, int64_t ws_size,
+                       hipStream_t s, const char* fn) {
+  int64_t ppb = 0;
+  int64_t chunks = spatial_chunks(xd, &ppb);
+  VAE2_REQUIRE(part && ws_size >= xd->n * chunks * xd->c, fn, "workspace too small");
+  hipLaunchKernelGGL(spatial_partials_kernel, dim3((unsigned)chunks, (unsigned)xd->n),
+                     dim3(256), 0, s, x, to_act(xd), ppb, part);
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  int64_t nc = xd->n * xd->c;
+  hipLaunchKernelGGL(spatial_finish_kernel, dim3((unsigned)ceil_div(nc, 256)), dim3(256), 0, s,
+                     (const float*)part, chunks, xd->n, xd->c, out, os, scale, accumulate);
+  return check_launch(fn);
+}
+
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ y, Act yd,
+                                                           float beta, FastDiv cdiv,
+                                                           FastDiv hwdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t HW = (uint32_t)(yd.h * yd.w);
+  const uint32_t total = (uint32_t)yd.n * HW * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    // i indexes the NCHW source linearly: coalesced reads
+    uint32_t nc = hwdiv.div(i);
+    uint32_t hw = i - nc * HW;
+    uint32_t n = cdiv.div(nc);
+    uint32_t c = nc - n * C;
+    float* dst = y + ((int64_t)n * HW + hw) * yd.ps + c;
+    float v = x[i];
+    *dst = (beta != 0.f) ? v + beta * *dst : v;
+  }
+}
+
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float* __restrict__ x, Act xd,
+                                                           float* __restrict__ y, float beta,
+                                                           FastDiv cdiv, FastDiv hwdiv) {
+  const uint32_t C = (uint32_t)xd.c;
+  const uint32_t HW = (uint32_t)(xd.h * xd.w);
+  const uint32_t total = (uint32_t)xd.n * HW * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t nc = hwdiv.div(i);
+    uint32_t hw = i - nc * HW;
+    uint32_t n = cdiv.div(nc);
+    uint32_t c = nc - n * C;
+    float v = x[((int64_t)n * HW + hw) * xd.ps + c];
+    y[i] = (beta != 0.f) ? v + beta * y[i] : v;
+  }
+}
+
+static bool same_hw(const vae2_act* a, const vae2_act* b) {
+  return a->n == b->n && a->h == b->h && a->w == b->w;
+}
+
+}  // namespace vae2
+
+using namespace vae2;
+
+extern "C" {
+
+int vae2_abi_version(void) { return VAE2_ABI_VERSION; }
+
+const char* vae2_last_error(void) { return g_last_error.c_str(); }
+
+int vae2_upsample_bilinear_fwd(const float* x, const vae2_act* xd, float* y,
+                               const vae2_act* yd, float beta, void* stream) {
+  const char* fn = "vae2_upsample_bilinear_fwd";
+  VAE2_REQUIRE(x && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(xd->n == yd->n && xd->c == yd->c, fn, "n / c mismatch");
+  int64_t total = act_elems(yd);
+  VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
+  hipLaunchKernelGGL(upsample_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+                     as_stream(stream), x, to_act(xd), y, to_act(yd), beta,
+                     FastDiv((uint32_t)yd->c), FastDiv((uint32_t)yd->w),
+                     FastDiv((uint32_t)yd->h));
+  return check_launch(fn);
+}
+
+int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
+                               const vae2_act* dxd, float beta, void* stream) {
+  const char* fn = "vae2_upsample_bilinear_bwd";
+  VAE2_REQUIRE(dy && dx && act_ok(dyd) && act_ok(dxd), fn, "bad arguments");
+  VAE2_REQUIRE(dxd->n == dyd->n && dxd->c == dyd->c, fn, "n / c mismatch");
+  int64_t total = act_elems(dxd);
+  VAE2_REQUIRE(total < (int64_t(1) << 31) && act_elems(dyd) < (int64_t(1) << 31), fn,
+               "tensor too large");
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+                     as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
+                     FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)dxd->w),
+                     FastDiv((uint32_t)dxd->h));
+  return check_launch(fn);
+}
+
+int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
+                       float* y, const vae2_act* yd, void* stream) {
+  const char* fn = "vae2_fuse_sum_relu";
+  VAE2_REQUIRE(n >= 1 && n <= 4 && xs && xds && y && act_ok(yd), fn, "bad arguments");
+  FuseTerms t{};
+  t.n = n;
+  for (int k = 0; k < n; ++k) {
+    VAE2_REQUIRE(xs[k] && act_ok(&xds[k]), fn, "bad term");
+    VAE2_REQUIRE(xds[k].n == yd->n && xds[k].c == yd->c, fn, "term n / c mismatch");
+    VAE2_REQUIRE(xds[k].h <= yd->h && xds[k].w <= yd->w, fn, "terms cannot be downsampled");
+    t.x[k] = xs[k];
+    t.d[k] = to_act(&xds[k]);
+  }
+  int64_t total = act_elems(yd);
+  VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
+  hipLaunchKernelGGL(fuse_sum_relu_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+                     as_stream(stream), t, y, to_act(yd), FastDiv((uint32_t)yd->c),
+                     FastDiv((uint32_t)yd->w), FastDiv((uint32_t)yd->h));
+  return check_launch(fn);
+}
+
+int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,
+                  const vae2_act* yd, float* g, const vae2_act* gd,
+                  void* stream) {
+  const char* fn = "vae2_relu_bwd";
+  VAE2_REQUIRE(dy && y && g && act_ok(dyd) && act_ok(yd) && act_ok(gd), fn, "bad arguments");
+  VAE2_REQUIRE(same_hw(dyd, yd) && same_hw(yd, gd) && dyd->c == yd->c && gd->c == yd->c, fn,
+               "shape mismatch");
+  int64_t total = act_elems(yd);
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+                     dy, to_act(dyd), y, to_act(yd), g, to_act(gd), FastDiv((uint32_t)yd->c));
+  return check_launch(fn);
+}
+
+int vae2_copy_act(const float* x, const vae2_act* xd, float* y,
+                  const vae2_act* yd, float beta, void* stream) {
+  const char* fn = "vae2_copy_act";
+  VAE2_REQUIRE(x && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(same_hw(xd, yd) && xd->c == yd->c, fn, "shape mismatch");
+  int64_t total = act_elems(xd);
+  hipLaunchKernelGGL(copy_act_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+                     x, to_act(xd), y, to_act(yd), beta, FastDiv((uint32_t)xd->c));
+  return check_launch(fn);
+}
+
+int vae2_codemap_tile_fwd(const float* v, int64_t vs, float* y,
+                          const vae2_act* yd, void* stream) {
+  const char* fn = "vae2_codemap_tile_fwd";
+  VAE2_REQUIRE(v && y && act_ok(yd) && vs >= yd->c, fn, "bad arguments");
+  int64_t total = act_elems(yd);
+  hipLaunchKernelGGL(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), v,
+                     vs, y, to_act(yd), 1.f, 0.f, FastDiv((uint32_t)yd->c),
+                     FastDiv((uint32_t)(yd->h * yd->w)));
+  return check_launch(fn);
+}
+
+int64_t vae2_spatial_ws_size(const vae2_act* xd) {
+  if (!act_ok(xd)) return 0;
+  return xd->n * spatial_chunks(xd, nullptr) * xd->c;
+}
+
+int vae2_codemap_tile_bwd(const float* dy, const vae2_act* dyd, float* dv,
+                          int64_t vs, int accumulate, float* ws, int64_t ws_size,
+                          void* stream) {
+  const char* fn = "vae2_codemap_tile_bwd";
+  VAE2_REQUIRE(dy && dv && act_ok(dyd) && vs >= dyd->c, fn, "bad arguments");
+  return spatial_sum(dy, dyd, dv, vs, 1.f, accumulate, ws, ws_size, as_stream(stream), fn);
+}
+
+int vae2_nchw_to_nhwc(const float* x, float* y, const vae2_act* yd,
+                      float beta, void* stream) {
+  const char* fn = "vae2_nchw_to_nhwc";
+  VAE2_REQUIRE(x && y && act_ok(yd), fn, "bad arguments");
+  int64_t total = act_elems(yd);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+                     as_stream(stream), x, y, to_act(yd), beta, FastDiv((uint32_t)yd->c),
+                     FastDiv((uint32_t)(yd->h * yd->w)));
+  return check_launch(fn);
+}
+
+int vae2_nhwc_to_nchw(const float* x, const vae2_act* xd, float* y,
+                      float beta, void* stream) {
+  const char* fn = "vae2_nhwc_to_nchw";
+  VAE2_REQUIRE(x && y && act_ok(xd), fn, "bad arguments");
+  int64_t total = act_elems(xd);
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+                     as_stream(stream), x, to_act(xd), y, beta, FastDiv((uint32_t)xd->c),
+                     FastDiv((uint32_t)(xd->h * xd->w)));
+  return check_launch(fn);
+}
+
+int vae2_global_avgpool_fwd(const float* x, const vae2_act* xd, float* y,
+                            const vae2_act* yd, float* ws, int64_t ws_size,
+                            void* stream) {
+  const char* fn = "vae2_global_avgpool_fwd";
+  VAE2_REQUIRE(x && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(yd->h == 1 && yd->w == 1 && yd->n == xd->n && yd->c == xd->c, fn,
+               "output must be (n, 1, 1, c)");
+  return spatial_sum(x, xd, y, yd->ps, 1.f / (float)(xd->h * xd->w), 0, ws, ws_size,
+                     as_stream(stream), fn);
+}
+
+int vae2_global_avgpool_bwd(const float* dy, const vae2_act* dyd, float* dx,
+                            const vae2_act* dxd, float beta, void* stream) {
+  const char* fn = "vae2_global_avgpool_bwd";
+  VAE2_REQUIRE(dy && dx && act_ok(dyd) && act_ok(dxd), fn, "bad arguments");
+  VAE2_REQUIRE(dyd->h == 1 && dyd->w == 1 && dyd->n == dxd->n && dyd->c == dxd->c, fn,
+               "dy must be (n, 1, 1, c)");
+  int64_t total = act_elems(dxd);
+  hipLaunchKernelGGL(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), dy,
+                     dyd->ps, dx, to_act(dxd), 1.f / (float)(dxd->h * dxd->w), beta,
+                     FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)(dxd->h * dxd->w)));
+  return check_launch(fn);
+}
+
+}  // extern "C"

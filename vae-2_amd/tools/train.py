@@ -1,0 +1,154 @@
+"""VAE² training CLI on MI355X (drop-in for the reference's tools/train.py).
+
+    python tools/train.py --cfg experiments/vae2_w18_small_v2_128x256.yaml [KEY VALUE ...]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/train.py --cfg ... GPUS "(0,1,2,3,4,5,6,7)"
+
+Flow (reference train.py:55-353): parse args + YAML -> logger -> models (same
+factories, same RNG order) -> process group (RCCL) -> dataset / sampler / loader
+-> FullModel_encdec -> SyncBN statistics + flat-gradient all-reduce (instead of
+DDP) -> Adam -> resume -> epoch loop -> rank-0 checkpoints with the reference's
+file and key names.
+
+Deliberate differences: `TRAIN.OPTIMIZER: sgd` raises a clear ValueError (the
+reference crashes with a TypeError on `p.name`, train.py:234); single-GPU
+checkpoints are written (the reference calls `.module` on a non-DDP model,
+train.py:322); the GAN / discriminator path (GAN_LAMBDA != 0) is not implemented
+yet; the Cityscapes zip dataset is replaced by MI355X.SYNTHETIC_DATA clips.
+"""
+import argparse
+import os
+import pprint
+import shutil
+import sys
+import timeit
+
+import torch
+
+import _init_paths  # noqa: F401
+import models  # noqa: F401
+from config import config, update_config
+from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
+from core.function import adversarial_train
+from utils.utils import FullModel_encdec, create_logger
+
+from vae2 import dist as vdist
+from vae2.optim import FusedAdam
+from vae2.trainer import NullWriter, SyntheticClips
+
+
+def parse_args(argv=None):
+    parser = argparse.ArgumentParser(description="Train VAE2 (MI355X)")
+    parser.add_argument("--cfg", help="experiment configure file name", required=True, type=str)
+    parser.add_argument("--local_rank", "--local-rank", type=int,
+                        default=int(os.environ.get("LOCAL_RANK", "0")))
+    parser.add_argument("opts", help="Modify config options using the command-line", default=None,
+                        nargs=argparse.REMAINDER)
+    args = parser.parse_args(argv)
+    update_config(config, args)
+    return args
+
+
+def build_dataset(cfg):
+    if cfg.MI355X.SYNTHETIC_DATA:
+        w, h = cfg.TRAIN.IMAGE_SIZE
+        return SyntheticClips(cfg.MI355X.SYNTHETIC_CLIPS, cfg.TRAIN.CLIP_LENGTH, h, w)
+    raise NotImplementedError(
+        "the Cityscapes zip clip dataset is SURVEY.md §8f next-2; set MI355X.SYNTHETIC_DATA True")
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    logger, final_output_dir, tb_log_dir = create_logger(config, args.cfg, "train")
+    logger.info(pprint.pformat(args))
+    logger.info(config)
+    writer_dict = {"writer": NullWriter(), "train_global_steps": 0, "valid_global_steps": 0}
+    try:
+        from tensorboardX import SummaryWriter
+        writer_dict["writer"] = SummaryWriter(tb_log_dir)
+    except ImportError:
+        logger.info("tensorboardX not installed: scalars are logged to the text log only")
+
+    gpus = list(config.GPUS)
+    distributed = len(gpus) > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if config.TRAIN.OPTIMIZER != "adam":
+        raise ValueError("Only Support ADAM optimizer (the reference's sgd path is broken)")
+    extra = config.MODEL.EXTRA
+
+    # models, in the reference's construction order (train.py:79-82)
+    encdec_model = models.enc_hrnet.get_encdec_model(config)
+    encz_model = (models.enc_hrnet.get_encz_model(config)
+                  if extra.BASELINE_MODE != "DETERMINISTIC" else None)
+    use_gan = config.TRAIN.GAN_LAMBDA != 0 and (not extra.IS_BASELINE
+                                                 or extra.BASELINE_MODE == "VAE_GAN")
+    D_model_sequence = models.enc_hrnet.get_D_sequence_model(config) if use_gan else None
+    D_model_frame = models.enc_hrnet.get_D_frame_model(config) if use_gan else None
+
+    if args.local_rank == 0:
+        this_dir = os.path.dirname(os.path.abspath(__file__))
+        dst = os.path.join(final_output_dir, "models")
+        if os.path.exists(dst):
+            shutil.rmtree(dst)
+        shutil.copytree(os.path.join(this_dir, "..", "lib", "models"), dst)
+
+    if distributed:
+        vdist.init("nccl")
+        vdist.set_sync_bn(config.MI355X.SYNC_BN)
+    device = torch.device("cuda:{}".format(args.local_rank))
+    torch.cuda.set_device(device)
+
+    dataset = build_dataset(config)
+    sampler = torch.utils.data.distributed.DistributedSampler(dataset) if vdist.is_dist() else None
+    loader = torch.utils.data.DataLoader(
+        dataset, batch_size=config.TRAIN.BATCH_SIZE_PER_GPU,
+        shuffle=config.TRAIN.SHUFFLE and sampler is None, num_workers=config.WORKERS,
+        pin_memory=True, drop_last=True, sampler=sampler)
+
+    model_encdec = FullModel_encdec(
+        encz_model=encz_model, encdec_model=encdec_model, D_model_sequence=D_model_sequence,
+        D_model_frame=D_model_frame, criterion_recon=L1Loss(), criterion_KL=KLLoss(),
+        criterion_gan=lsgan_adversarial_loss(), x1recon_lambda=config.TRAIN.X1RECON_LAMBDA,
+        x2recon_lambda=config.TRAIN.X2RECON_LAMBDA, x3recon_lambda=config.TRAIN.X3RECON_LAMBDA,
+        gan_lambda=config.TRAIN.GAN_LAMBDA)
+    model_encdec.defer_checks = config.MI355X.DEFER_CHECKS
+    model_encdec = model_encdec.to(device)
+    nets = [m for m in (encz_model, encdec_model) if m is not None]
+    optimizer = FusedAdam(nets, lr=config.TRAIN.LR)
+    if vdist.is_dist():  # replicas start identical (DDP's initial broadcast)
+        for f in optimizer.flats:
+            torch.distributed.broadcast(f.data, src=0)
+
+    epoch_iters = int(len(dataset) / config.TRAIN.BATCH_SIZE_PER_GPU / max(1, len(gpus)))
+    last_epoch = 0
+    state_file = os.path.join(final_output_dir, "checkpoint_encdec.pth.tar")
+    if config.TRAIN.RESUME and os.path.isfile(state_file):
+        ck = torch.load(state_file, map_location="cpu", weights_only=True)
+        last_epoch = ck["epoch"]
+        model_encdec.load_state_dict(ck["state_dict"], strict=False)
+        optimizer.load_state_dict(ck["optimizer_encdec"])
+        logger.info("=> loaded checkpoint (epoch {})".format(ck["epoch"]))
+
+    start = timeit.default_timer()
+    end_epoch = config.TRAIN.END_EPOCH + config.TRAIN.EXTRA_EPOCH
+    num_iters = config.TRAIN.END_EPOCH * epoch_iters
+    for epoch in range(last_epoch, end_epoch):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        adversarial_train(config, epoch, config.TRAIN.END_EPOCH, epoch_iters, config.TRAIN.LR,
+                          num_iters, loader, optimizer, None, model_encdec, None, writer_dict,
+                          device, final_output_dir,
+                          use_multiplier=config.TRAIN.USE_X2RECON_MULTIPLIER,
+                          is_baseline=extra.IS_BASELINE, baseline_mode=extra.BASELINE_MODE)
+        if vdist.rank() == 0:
+            logger.info("=> saving checkpoint to {}".format(state_file))
+            torch.save({"epoch": epoch + 1, "state_dict": model_encdec.state_dict(),
+                        "optimizer_encdec": optimizer.state_dict()}, state_file)
+            if epoch == end_epoch - 1:
+                torch.save(model_encdec.state_dict(),
+                           os.path.join(final_output_dir, "model_encdec_final_state.pth"))
+                writer_dict["writer"].close()
+                logger.info("Hours: %d" % int((timeit.default_timer() - start) / 3600))
+                logger.info("Done")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

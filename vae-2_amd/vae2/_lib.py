@@ -1,0 +1,122 @@
+"""ctypes binding of libvae2_hip.so (the C ABI declared in include/vae2_hip.h).
+
+The product path has exactly one compute backend: the HIP kernels in this
+library.  Loading fails loudly when the library is missing; there is no CPU or
+eager-PyTorch fallback.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads PyTorch's libamdhip64 first: one HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VAE2_LIB", os.path.join(_HERE, "libvae2_hip.so"))
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_vp = ctypes.c_void_p
+
+
+class Act(ctypes.Structure):
+    """vae2_act: NHWC view, element (n,y,x,c) at ptr[((n*h+y)*w+x)*ps + c]."""
+
+    _fields_ = [("n", c_i64), ("h", c_i64), ("w", c_i64), ("c", c_i64), ("ps", c_i64)]
+
+
+P_ACT = ctypes.POINTER(Act)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "vae2_abi_version": (c_int, []),
+    "vae2_last_error": (ctypes.c_char_p, []),
+    "vae2_conv2d_fwd_stats_rows": (c_i64, [P_ACT, c_i64]),
+    "vae2_conv2d_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
+                                c_f32, c_vp, c_vp]),
+    "vae2_conv2d_fwd_kernel_name": (c_int, [P_ACT, c_i64, ctypes.c_char_p, c_i64]),
+    "vae2_conv2d_bwd_data": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
+                                     c_f32, c_vp]),
+    "vae2_conv2d_bwd_weight_ws_size": (c_i64, [P_ACT, P_ACT, c_int]),
+    "vae2_conv2d_bwd_weight": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_vp, c_int, c_int,
+                                       c_int, c_int, c_vp, c_i64, c_vp]),
+    "vae2_bn_partial_rows": (c_i64, [P_ACT]),
+    "vae2_bn_stats": (c_int, [c_vp, P_ACT, c_vp, c_vp]),
+    "vae2_bn_partials_reduce": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_vp]),
+    "vae2_bn_finalize": (c_int, [c_vp, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32,
+                                 c_i64, c_vp, c_vp]),
+    "vae2_bn_eval_coeffs": (c_int, [c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_vp, c_vp]),
+    "vae2_bn_apply": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_vp, P_ACT, c_int, c_vp]),
+    "vae2_bn_relu_bwd_reduce": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, c_int,
+                                        c_vp, c_vp]),
+    "vae2_bn_bwd_param_grads": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "vae2_bn_relu_bwd_apply": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, c_vp,
+                                       c_vp, c_f64, c_int, c_vp, P_ACT, c_vp, P_ACT, c_vp]),
+    "vae2_upsample_bilinear_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_upsample_bilinear_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_fuse_sum_relu": (c_int, [c_int, ctypes.POINTER(c_vp), P_ACT, c_vp, P_ACT, c_vp]),
+    "vae2_relu_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp]),
+    "vae2_copy_act": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_codemap_tile_fwd": (c_int, [c_vp, c_i64, c_vp, P_ACT, c_vp]),
+    "vae2_spatial_ws_size": (c_i64, [P_ACT]),
+    "vae2_codemap_tile_bwd": (c_int, [c_vp, P_ACT, c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
+    "vae2_nchw_to_nhwc": (c_int, [c_vp, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_nhwc_to_nchw": (c_int, [c_vp, P_ACT, c_vp, c_f32, c_vp]),
+    "vae2_global_avgpool_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_i64, c_vp]),
+    "vae2_global_avgpool_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_reduce_ws_size": (c_i64, [c_i64]),
+    "vae2_l1_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp, c_vp, c_vp]),
+    "vae2_l1_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_f32, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_reparam_kl_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_int, c_f32, c_vp,
+                                    c_int, c_vp, c_vp]),
+    "vae2_reparam_kl_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, c_f32, c_vp,
+                                    P_ACT, c_vp]),
+    "vae2_weighted_sum": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_f32), c_vp,
+                                  c_vp]),
+    "vae2_nonfinite_check": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "vae2_adam_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
+                               c_i64, c_vp]),
+    "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+def load():
+    """Load (once) and type the shared library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libvae2_hip.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no fallback compute path)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.vae2_abi_version() != ABI_VERSION:
+        raise RuntimeError("libvae2_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().vae2_last_error()
+        raise HipError(f"libvae2_hip error {rc}: {msg.decode() if msg else ''}")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args))

@@ -1,0 +1,84 @@
+"""Data-parallel runtime: RCCL gradient all-reduce and SyncBatchNorm statistics.
+
+Replaces DistributedDataParallel + nn.SyncBatchNorm.convert_sync_batchnorm
+(tools/train.py:107-111, :216-229) and reduce_tensor (function.py:32-43).
+One process per GPU; the "nccl" backend of PyTorch-ROCm is RCCL over xGMI.
+
+* SyncBN: every BatchNorm forward all-reduces its per-channel (sum x, sum x^2)
+  doubles, every backward its (sum g, sum g*xhat) doubles, so statistics are
+  global exactly as with SyncBatchNorm; parameter gradients use local sums and
+  are averaged by the gradient all-reduce, as DDP does.
+* Gradients: the flat gradient buffer of each model is all-reduced (sum) in
+  buckets and scaled by 1/world in a HIP kernel (DDP's mean).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from ._lib import call
+
+_SYNC_BN_GROUP = None
+_SYNC_BN = False
+
+
+def is_dist():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_size():
+    return dist.get_world_size() if is_dist() else 1
+
+
+def rank():
+    return dist.get_rank() if is_dist() else 0
+
+
+def init(backend=None):
+    """Initialise the process group from torchrun's env (MASTER_ADDR/PORT, RANK, WORLD_SIZE)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend, init_method="env://")
+
+
+def set_sync_bn(enabled, group=None):
+    """Enable global batch statistics (the reference's SyncBatchNorm conversion)."""
+    global _SYNC_BN, _SYNC_BN_GROUP
+    _SYNC_BN = bool(enabled)
+    _SYNC_BN_GROUP = group
+
+
+def sync_bn_group():
+    if not _SYNC_BN or not is_dist():
+        return None
+    return _SYNC_BN_GROUP if _SYNC_BN_GROUP is not None else dist.group.WORLD
+
+
+BUCKET_ELEMS = 8 * 1024 * 1024  # 32 MB fp32 buckets
+
+
+def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
+    """Mean-reduce the flat gradient buffers over all ranks."""
+    if not is_dist():
+        return
+    ws = world_size()
+    for f in flats:
+        g = f.grad
+        n = g.numel()
+        for off in range(0, n, bucket_elems):
+            dist.all_reduce(g[off:off + bucket_elems])
+        call("vae2_scale", ops.ptr(g), ops.ptr(g), n, 1.0 / ws, ops.stream_ptr())
+
+
+def reduce_tensor(inp):
+    """dist.reduce(sum) to rank 0 (function.py:32-43)."""
+    if world_size() < 2:
+        return inp
+    with torch.no_grad():
+        dist.reduce(inp, dst=0)
+    return inp

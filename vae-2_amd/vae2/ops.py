@@ -1,0 +1,661 @@
+"""Autograd operators of the VAE² ELBO step, each backed by libvae2_hip kernels.
+
+Activations are NHWC fp32 device tensors of shape (N, H, W, C) whose channel
+axis is contiguous (channel slices of a wider buffer are allowed: every kernel
+takes the pixel stride).  Parameters keep the reference nn.Conv2d /
+nn.BatchNorm2d layouts.
+
+Gradients of parameters that carry a ``main_grad`` attribute (the flat gradient
+buffer set up by :mod:`vae2.params`) are accumulated straight into it by the
+kernels; parameters without one receive ordinary autograd gradients.
+
+Reference operators replaced (see include/vae2_hip.h for the kernel entry points):
+  conv_bn     nn.Conv2d -> nn.BatchNorm2d -> [+residual] -> [nn.ReLU]
+              (BasicBlock/Bottleneck enc_hrnet.py:33-103, stems :465-470/:788-793,
+              transitions :372-406, fuse branches :177-221, heads :323-370)
+  conv        nn.Conv2d with bias, no BN (final head conv, z-net head :1024-1040)
+  fuse_sum    HighResolutionModule fuse sum + bilinear upsample + ReLU :233-249
+  up_cat      F.upsample(bilinear) of branches 1..3 + torch.cat :833-839
+  cat         torch.cat on channels incl. code-map tiling :454-462, :818-830
+  avgpool     nn.AdaptiveAvgPool2d((1, 1)) :1025
+  l1          L1Loss criterion.py:61-69
+  reparam_kl  z = mu + exp(0.5 logvar) eps (utils.py:85-101) + KLLoss criterion.py:72-87
+  weighted_sum  loss assembly utils.py:150-152
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, prof
+from ._lib import Act, call
+
+_F32 = torch.float32
+
+
+# ----------------------------------------------------------------- helpers ----
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def act_of(t):
+    """(data pointer, Act) of an NHWC activation view."""
+    if t.dim() != 4 or t.dtype != _F32 or not t.is_cuda:
+        raise ValueError(f"expected a 4-D float32 device tensor (N,H,W,C), got {tuple(t.shape)} "
+                         f"{t.dtype} on {t.device}")
+    n, h, w, c = t.shape
+    s0, s1, s2, s3 = t.stride()
+    if c > 1 and s3 != 1:
+        raise ValueError("channel axis must be contiguous")
+    if w > 1:
+        ps = s2
+    elif h > 1:
+        ps = s1
+    elif n > 1:
+        ps = s0
+    else:
+        ps = c
+    if (w > 1 and s2 != ps) or (h > 1 and s1 != w * ps) or (n > 1 and s0 != h * w * ps) or ps < c:
+        raise ValueError(f"not a uniform NHWC view: shape {tuple(t.shape)} strides {t.stride()}")
+    return ctypes.c_void_p(t.data_ptr()), Act(n, h, w, c, ps)
+
+
+def as_act(t):
+    """Return t if it is an NHWC view the kernels accept, else a contiguous copy."""
+    try:
+        act_of(t)
+        return t
+    except ValueError:
+        return t.contiguous()
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _empty(shape, like, dtype=_F32):
+    return torch.empty(shape, dtype=dtype, device=like.device)
+
+
+def _grad_sink(p):
+    """(buffer to accumulate a parameter gradient into, value autograd should get)."""
+    if p is None or not p.requires_grad:
+        return None, None
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        return mg, None
+    g = torch.zeros_like(p)
+    return g, g
+
+
+def _bn_group():
+    from . import dist as vdist
+    return vdist.sync_bn_group()
+
+
+def _all_reduce_sums(sums, count, group):
+    if group is None:
+        return sums, count
+    out = sums.clone()
+    dist.all_reduce(out, group=group)
+    return out, count * dist.get_world_size(group)
+
+
+# --------------------------------------------------------------- conv + BN ----
+class ConvSpec:
+    """Static description of a conv(+BN) call: geometry and module handles."""
+
+    __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training")
+
+    def __init__(self, conv, bn=None, relu=False):
+        kh, kw = conv.kernel_size
+        if kh != kw or conv.stride[0] != conv.stride[1] or conv.padding[0] != conv.padding[1]:
+            raise ValueError("only square kernels / strides / paddings are used by the model")
+        if conv.groups != 1 or conv.dilation != (1, 1):
+            raise ValueError("grouped / dilated convs are not used by the model")
+        self.k, self.stride, self.pad = kh, conv.stride[0], conv.padding[0]
+        self.relu = relu
+        self.bn = bn
+        if bn is not None:
+            if bn.momentum is None:
+                raise ValueError("cumulative-average BatchNorm (momentum=None) is not supported")
+            self.momentum = float(bn.momentum)
+            self.eps = float(bn.eps)
+            self.training = bn.training or not bn.track_running_stats
+        else:
+            self.momentum = self.eps = 0.0
+            self.training = False
+
+    def out_hw(self, h, w):
+        return ((h + 2 * self.pad - self.k) // self.stride + 1,
+                (w + 2 * self.pad - self.k) // self.stride + 1)
+
+
+def _conv_fwd(x, weight, bias, spec, stats=None):
+    xp, xa = act_of(x)
+    n, h, w, _ = x.shape
+    oh, ow = spec.out_hw(h, w)
+    cout = weight.shape[0]
+    y = _empty((n, oh, ow, cout), x)
+    yp, ya = act_of(y)
+    timer = prof.active()
+    ev = None
+    if timer is not None and timer.matches(n, oh, ow, cout):
+        ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k)
+    call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(weight), ptr(bias), yp, ctypes.byref(ya),
+         spec.k, spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
+    if ev is not None:
+        ev.record(torch.cuda.current_stream())
+    return y
+
+
+def _conv_bwd(x, weight, bias, dy, spec, need_dx):
+    """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b)."""
+    s = stream_ptr()
+    xp, xa = act_of(x)
+    dyp, dya = act_of(dy)
+    wsink, wret = _grad_sink(weight)
+    bsink, bret = _grad_sink(bias)
+    if wsink is not None or bsink is not None:
+        if wsink is None:  # weight frozen but bias trained: still need a dW target
+            wsink = torch.zeros_like(weight)
+        size = _lib.load().vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xa), ctypes.byref(dya),
+                                                          spec.k)
+        ws = _empty((max(size, 1),), x)
+        call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya), ptr(wsink),
+             ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
+    dx = None
+    if need_dx:
+        dx = _empty(tuple(x.shape), x)
+        dxp, dxa = act_of(dx)
+        call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(weight), dxp, ctypes.byref(dxa),
+             spec.k, spec.stride, spec.pad, 0.0, s)
+    return dx, wret, bret
+
+
+class _ConvBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, residual, spec):
+        lib = _lib.load()
+        s = stream_ptr()
+        bn = spec.bn
+        n, h, w, _ = x.shape
+        oh, ow = spec.out_hw(h, w)
+        cout = weight.shape[0]
+        count = float(n * oh * ow)
+        group = None
+        if spec.training:
+            rows = lib.vae2_conv2d_fwd_stats_rows(ctypes.byref(Act(n, oh, ow, cout, cout)), cout)
+            stats = _empty((2 * rows * cout,), x)
+            r = _conv_fwd(x, weight, bias, spec, stats)
+            sums = _empty((2 * cout,), x, torch.float64)
+            call("vae2_bn_partials_reduce", ptr(stats), rows, cout, ptr(sums), 0, s)
+            group = _bn_group()
+            sums, count = _all_reduce_sums(sums, count, group)
+            save = _empty((4 * cout,), x)
+            track = bn.track_running_stats and bn.running_mean is not None
+            call("vae2_bn_finalize", ptr(sums), count, ptr(gamma), ptr(beta),
+                 ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
+                 ptr(bn.num_batches_tracked) if track else None, spec.momentum, spec.eps, cout,
+                 ptr(save), s)
+        else:
+            r = _conv_fwd(x, weight, bias, spec)
+            save = _empty((4 * cout,), x)
+            call("vae2_bn_eval_coeffs", ptr(gamma), ptr(beta), ptr(bn.running_mean),
+                 ptr(bn.running_var), spec.eps, cout, ptr(save), s)
+        y = _empty((n, oh, ow, cout), x)
+        rp, ra = act_of(r)
+        yp, ya = act_of(y)
+        if residual is not None:
+            resp, resa = act_of(residual)
+        else:
+            resp, resa = None, ya
+        call("vae2_bn_apply", rp, ctypes.byref(ra), ptr(save), resp, ctypes.byref(resa), yp,
+             ctypes.byref(ya), int(spec.relu), s)
+        ctx.spec = spec
+        ctx.count = count
+        ctx.group = group
+        ctx.has_res = residual is not None
+        ctx.params = (weight, bias, gamma, beta)
+        ctx.save_for_backward(x, r, y, save)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if not ctx.spec.training:
+            raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
+        lib = _lib.load()
+        s = stream_ptr()
+        x, r, y, save = ctx.saved_tensors
+        weight, bias, gamma, beta = ctx.params
+        spec = ctx.spec
+        dy = as_act(dy)
+        cout = r.shape[3]
+        dyp, dya = act_of(dy)
+        rp, ra = act_of(r)
+        yp, ya = act_of(y)
+        rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
+        part = _empty((2 * rows * cout,), r)
+        call("vae2_bn_relu_bwd_reduce", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
+             ctypes.byref(ra), ptr(save), int(spec.relu), ptr(part), s)
+        lsums = _empty((2 * cout,), r, torch.float64)
+        call("vae2_bn_partials_reduce", ptr(part), rows, cout, ptr(lsums), 0, s)
+        gsink, gret = _grad_sink(gamma)
+        bsink, bret = _grad_sink(beta)
+        if gsink is not None or bsink is not None:
+            call("vae2_bn_bwd_param_grads", ptr(lsums), cout, ptr(gsink), ptr(bsink), s)
+        gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
+        dr = _empty(tuple(r.shape), r)
+        drp, dra = act_of(dr)
+        dres = None
+        if ctx.has_res and ctx.needs_input_grad[5]:
+            dres = _empty(tuple(r.shape), r)
+            dresp, dresa = act_of(dres)
+        else:
+            dresp, dresa = None, dra
+        call("vae2_bn_relu_bwd_apply", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
+             ctypes.byref(ra), ptr(save), ptr(gamma), ptr(gsums), ctx.count, int(spec.relu), drp,
+             ctypes.byref(dra), dresp, ctypes.byref(dresa), s)
+        dx, wret, bret_conv = _conv_bwd(x, weight, bias, dr, spec, ctx.needs_input_grad[0])
+        return dx, wret, bret_conv, gret, bret, dres, None
+
+
+def conv_bn(x, conv, bn, relu, residual=None):
+    """relu?(bn(conv(x)) + residual) with training-mode (or eval-mode) BatchNorm."""
+    spec = ConvSpec(conv, bn, relu)
+    return _ConvBN.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec)
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, spec):
+        y = _conv_fwd(x, weight, bias, spec)
+        ctx.spec = spec
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        weight, bias = ctx.params
+        dx, wret, bret = _conv_bwd(x, weight, bias, as_act(dy), ctx.spec, ctx.needs_input_grad[0])
+        return dx, wret, bret, None
+
+
+def conv(x, conv_mod):
+    """nn.Conv2d forward (with its bias), no normalisation."""
+    return _Conv.apply(x, conv_mod.weight, conv_mod.bias, ConvSpec(conv_mod))
+
+
+# ------------------------------------------------------------- fuse / cat ----
+def _up_bwd(g, shape):
+    dx = _empty(shape, g)
+    gp, ga = act_of(g)
+    dxp, dxa = act_of(dx)
+    call("vae2_upsample_bilinear_bwd", gp, ctypes.byref(ga), dxp, ctypes.byref(dxa), 0.0,
+         stream_ptr())
+    return dx
+
+
+class _FuseSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out_hw, *terms):
+        ref = terms[0]
+        n, c = ref.shape[0], ref.shape[3]
+        y = _empty((n, out_hw[0], out_hw[1], c), ref)
+        ptrs = (ctypes.c_void_p * len(terms))()
+        acts = (Act * len(terms))()
+        for i, t in enumerate(terms):
+            p_, a_ = act_of(t)
+            ptrs[i] = p_
+            acts[i] = a_
+        yp, ya = act_of(y)
+        call("vae2_fuse_sum_relu", len(terms), ptrs, acts, yp, ctypes.byref(ya), stream_ptr())
+        ctx.shapes = [tuple(t.shape) for t in terms]
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = as_act(dy)
+        g = _empty(tuple(y.shape), y)
+        dyp, dya = act_of(dy)
+        yp, ya = act_of(y)
+        gp, ga = act_of(g)
+        call("vae2_relu_bwd", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), gp, ctypes.byref(ga),
+             stream_ptr())
+        grads = []
+        for i, shp in enumerate(ctx.shapes):
+            if not ctx.needs_input_grad[i + 1]:
+                grads.append(None)
+            elif shp[1:3] == tuple(y.shape[1:3]):
+                grads.append(g)
+            else:
+                grads.append(_up_bwd(g, shp))
+        return (None, *grads)
+
+
+def fuse_sum_relu(terms, out_hw):
+    """relu(sum of terms), lower-resolution terms bilinearly upsampled to out_hw."""
+    return _FuseSum.apply(tuple(out_hw), *terms)
+
+
+class _UpCat(torch.autograd.Function):
+    """cat([x0, up(x1), up(x2), ...], channels) at x0's resolution."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        x0 = xs[0]
+        n, h, w, _ = x0.shape
+        ctot = sum(t.shape[3] for t in xs)
+        y = _empty((n, h, w, ctot), x0)
+        s = stream_ptr()
+        off = 0
+        for t in xs:
+            c = t.shape[3]
+            dst = y[..., off:off + c]
+            tp, ta = act_of(t)
+            dp_, da = act_of(dst)
+            if t.shape[1:3] == x0.shape[1:3]:
+                call("vae2_copy_act", tp, ctypes.byref(ta), dp_, ctypes.byref(da), 0.0, s)
+            else:
+                call("vae2_upsample_bilinear_fwd", tp, ctypes.byref(ta), dp_, ctypes.byref(da), 0.0,
+                     s)
+            off += c
+        ctx.shapes = [tuple(t.shape) for t in xs]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = as_act(dy)
+        grads = []
+        off = 0
+        for i, shp in enumerate(ctx.shapes):
+            c = shp[3]
+            sl = dy[..., off:off + c]
+            off += c
+            if not ctx.needs_input_grad[i]:
+                grads.append(None)
+            elif shp[1:3] == tuple(dy.shape[1:3]):
+                grads.append(sl)
+            else:
+                grads.append(_up_bwd(sl, shp))
+        return tuple(grads)
+
+
+def up_cat(xs):
+    return _UpCat.apply(*xs)
+
+
+class _Cat(torch.autograd.Function):
+    """Channel concat of NHWC maps and per-clip vectors tiled over space.
+
+    parts: tensors that are either NHWC maps (N,h,w,c) at the output resolution or
+    per-clip vectors given as (N,1,1,c) maps with tile=True.
+    """
+
+    @staticmethod
+    def forward(ctx, out_hw, tiles, *parts):
+        ref = parts[0]
+        n = ref.shape[0]
+        ctot = sum(p_.shape[3] for p_ in parts)
+        y = _empty((n, out_hw[0], out_hw[1], ctot), ref)
+        s = stream_ptr()
+        off = 0
+        for p_, tile in zip(parts, tiles):
+            c = p_.shape[3]
+            dst = y[..., off:off + c]
+            dp_, da = act_of(dst)
+            pp, pa = act_of(p_)
+            if tile:
+                call("vae2_codemap_tile_fwd", pp, pa.ps, dp_, ctypes.byref(da), s)
+            else:
+                call("vae2_copy_act", pp, ctypes.byref(pa), dp_, ctypes.byref(da), 0.0, s)
+            off += c
+        ctx.tiles = tiles
+        ctx.shapes = [tuple(p_.shape) for p_ in parts]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = as_act(dy)
+        grads = []
+        off = 0
+        lib = _lib.load()
+        for i, (shp, tile) in enumerate(zip(ctx.shapes, ctx.tiles)):
+            c = shp[3]
+            sl = dy[..., off:off + c]
+            off += c
+            if not ctx.needs_input_grad[i + 2]:
+                grads.append(None)
+            elif tile:
+                g = _empty(shp, dy)
+                sp, sa = act_of(sl)
+                wsz = lib.vae2_spatial_ws_size(ctypes.byref(sa))
+                ws = _empty((max(wsz, 1),), dy)
+                gp, ga = act_of(g)
+                call("vae2_codemap_tile_bwd", sp, ctypes.byref(sa), gp, ga.ps, 0, ptr(ws), wsz,
+                     stream_ptr())
+                grads.append(g)
+            else:
+                grads.append(sl)
+        return (None, None, *grads)
+
+
+def cat(parts, out_hw, tiles=None):
+    tiles = tuple(tiles) if tiles is not None else (False,) * len(parts)
+    return _Cat.apply(tuple(out_hw), tiles, *parts)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, h, w, c = x.shape
+        y = _empty((n, 1, 1, c), x)
+        xp, xa = act_of(x)
+        yp, ya = act_of(y)
+        wsz = _lib.load().vae2_spatial_ws_size(ctypes.byref(xa))
+        ws = _empty((max(wsz, 1),), x)
+        call("vae2_global_avgpool_fwd", xp, ctypes.byref(xa), yp, ctypes.byref(ya), ptr(ws), wsz,
+             stream_ptr())
+        ctx.shape = tuple(x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = as_act(dy)
+        dx = _empty(ctx.shape, dy)
+        dyp, dya = act_of(dy)
+        dxp, dxa = act_of(dx)
+        call("vae2_global_avgpool_bwd", dyp, ctypes.byref(dya), dxp, ctypes.byref(dxa), 0.0,
+             stream_ptr())
+        return dx
+
+
+def avgpool(x):
+    return _AvgPool.apply(x)
+
+
+# ---------------------------------------------------------------- layout ----
+class _ToNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        y = _empty((n, h, w, c), x)
+        yp, ya = act_of(y)
+        call("vae2_nchw_to_nhwc", ptr(x), yp, ctypes.byref(ya), 0.0, stream_ptr())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = as_act(dy)
+        n, h, w, c = dy.shape
+        dx = _empty((n, c, h, w), dy)
+        dyp, dya = act_of(dy)
+        call("vae2_nhwc_to_nchw", dyp, ctypes.byref(dya), ptr(dx), 0.0, stream_ptr())
+        return dx
+
+
+class _ToNCHW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, h, w, c = x.shape
+        y = _empty((n, c, h, w), x)
+        xp, xa = act_of(x)
+        call("vae2_nhwc_to_nchw", xp, ctypes.byref(xa), ptr(y), 0.0, stream_ptr())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        n, c, h, w = dy.shape
+        dx = _empty((n, h, w, c), dy)
+        dxp, dxa = act_of(dx)
+        call("vae2_nchw_to_nhwc", ptr(dy), dxp, ctypes.byref(dxa), 0.0, stream_ptr())
+        return dx
+
+
+def to_nhwc(x):
+    return _ToNHWC.apply(x)
+
+
+def to_nchw(x):
+    return _ToNCHW.apply(x)
+
+
+# ------------------------------------------------------------------ ELBO ----
+def _flat_act(t):
+    """Describe a dense tensor of any layout as an (1,1,numel,1) activation (for
+    element-wise-and-sum kernels whose result does not depend on layout)."""
+    t = t.contiguous()
+    return t, Act(1, 1, t.numel(), 1, 1)
+
+
+class _L1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p, t, scale, flat):
+        if flat:
+            p, pa = _flat_act(p)
+            t, ta = _flat_act(t)
+            pp, tp = ptr(p), ptr(t)
+        else:
+            pp, pa = act_of(p)
+            tp, ta = act_of(t)
+        n = pa.n * pa.h * pa.w * pa.c
+        ws = _empty((_lib.load().vae2_reduce_ws_size(n),), p)
+        out = _empty((), p)
+        call("vae2_l1_fwd", pp, ctypes.byref(pa), tp, ctypes.byref(ta), scale, ptr(ws), ptr(out),
+             stream_ptr())
+        ctx.scale = scale
+        ctx.flat = flat
+        ctx.save_for_backward(p, t)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        p, t = ctx.saved_tensors
+        gout = gout.contiguous()
+        if ctx.flat:
+            _, pa = _flat_act(p)
+            _, ta = _flat_act(t)
+            dp = torch.empty_like(p)
+            _, da = _flat_act(dp)
+            pp, tp, dpp = ptr(p), ptr(t), ptr(dp)
+        else:
+            pp, pa = act_of(p)
+            tp, ta = act_of(t)
+            dp = _empty(tuple(p.shape), p)
+            dpp, da = act_of(dp)
+        call("vae2_l1_bwd", pp, ctypes.byref(pa), tp, ctypes.byref(ta), ptr(gout), ctx.scale, dpp,
+             ctypes.byref(da), 0.0, stream_ptr())
+        return dp, None, None, None
+
+
+def l1(pred, target, scale, flat=False):
+    """scale * sum |pred - target| (NHWC views, or any dense layout with flat=True)."""
+    return _L1.apply(pred, target, float(scale), flat)
+
+
+class _ReparamKL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, muvar, eps, prior, scale):
+        n, h, w, c2 = muvar.shape
+        zc = c2 // 2
+        z = _empty((n, h, w, zc), muvar)
+        kl = _empty((), muvar)
+        mp, ma = act_of(muvar)
+        ep, ea = act_of(eps)
+        zp, za = act_of(z)
+        ws = _empty((_lib.load().vae2_reduce_ws_size(n * h * w * zc),), muvar)
+        call("vae2_reparam_kl_fwd", mp, ctypes.byref(ma), ep, ctypes.byref(ea), zp, ctypes.byref(za),
+             int(prior), scale, ptr(kl), 0, ptr(ws), stream_ptr())
+        ctx.scale = scale
+        ctx.prior = prior
+        ctx.save_for_backward(muvar, eps)
+        return z, kl
+
+    @staticmethod
+    def backward(ctx, dz, dkl):
+        muvar, eps = ctx.saved_tensors
+        dm = _empty(tuple(muvar.shape), muvar)
+        mp, ma = act_of(muvar)
+        ep, ea = act_of(eps)
+        dmp, dma = act_of(dm)
+        if dz is not None and not ctx.prior:
+            dz = as_act(dz)
+            dzp, dza = act_of(dz)
+        else:
+            dzp, dza = None, ea
+        gk = dkl.contiguous() if dkl is not None else None
+        call("vae2_reparam_kl_bwd", mp, ctypes.byref(ma), ep, ctypes.byref(ea), dzp, ctypes.byref(dza),
+             ptr(gk), ctx.scale, dmp, ctypes.byref(dma), stream_ptr())
+        return dm, None, None, None
+
+
+def reparam_kl(muvar, eps, prior=False, scale=1.0):
+    """(z, KL): z = mu + exp(0.5 logvar) eps (or eps when prior), KL*scale."""
+    return _ReparamKL.apply(muvar, eps, bool(prior), float(scale))
+
+
+class _WeightedSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lambdas, *terms):
+        n = len(terms)
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in terms])
+        lams = (ctypes.c_float * n)(*lambdas)
+        out = _empty((), terms[0])
+        call("vae2_weighted_sum", n, ptrs, lams, ptr(out), stream_ptr())
+        ctx.lambdas = lambdas
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        grads = []
+        for i, lam in enumerate(ctx.lambdas):
+            if not ctx.needs_input_grad[i + 1]:
+                grads.append(None)
+                continue
+            d = torch.empty_like(g)
+            call("vae2_scale", ptr(d), ptr(g), 1, float(lam), stream_ptr())
+            grads.append(d)
+        return (None, *grads)
+
+
+def weighted_sum(terms, lambdas):
+    return _WeightedSum.apply(tuple(float(x) for x in lambdas), *terms)
+
+
+def nonfinite_flag(tensors, flag=None):
+    """Device flag (int32) set when any tensor holds a NaN/Inf (no host sync)."""
+    if flag is None:
+        flag = torch.zeros((1,), dtype=torch.int32, device=tensors[0].device)
+    for t in tensors:
+        t = t.detach()
+        if not t.is_contiguous():
+            t = t.contiguous()
+        call("vae2_nonfinite_check", ptr(t), t.numel(), ptr(flag), stream_ptr())
+    return flag

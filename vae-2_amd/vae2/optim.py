@@ -1,0 +1,88 @@
+"""Adam over flat parameter buffers (torch.optim.Adam semantics, train.py:251-261).
+
+One vae2_adam_step launch per flat buffer; the math follows torch.optim.Adam
+(lerp first moment, L2 weight decay folded into the gradient, bias corrections
+on the host).  state_dict() / load_state_dict() use torch.optim.Adam's format
+(per-parameter exp_avg / exp_avg_sq / step) so optimizer checkpoints interchange.
+"""
+import ctypes
+
+import torch
+
+from . import ops
+from ._lib import call
+from .params import flatten
+
+
+class FusedAdam:
+    def __init__(self, modules, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if not isinstance(modules, (list, tuple)):
+            modules = [modules]
+        self.flats = [flatten(m) for m in modules]
+        self.lr = float(lr)
+        self.betas = (float(betas[0]), float(betas[1]))
+        self.eps = float(eps)
+        self.weight_decay = float(weight_decay)
+        self.step_count = 0
+        self.exp_avg = [torch.zeros_like(f.data) for f in self.flats]
+        self.exp_avg_sq = [torch.zeros_like(f.data) for f in self.flats]
+        self.param_groups = [{"params": [p for f in self.flats for p in f.params], "lr": self.lr,
+                              "betas": self.betas, "eps": self.eps,
+                              "weight_decay": self.weight_decay, "amsgrad": False,
+                              "maximize": False, "foreach": None, "capturable": False,
+                              "differentiable": False, "fused": None}]
+
+    def zero_grad(self, set_to_none=False):
+        for f in self.flats:
+            f.zero_grad()
+
+    @torch.no_grad()
+    def step(self):
+        self.lr = float(self.param_groups[0]["lr"])
+        self.step_count += 1
+        s = ops.stream_ptr()
+        for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
+            call("vae2_adam_step", ops.ptr(f.data), ops.ptr(f.grad), ops.ptr(m), ops.ptr(v),
+                 f.numel, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
+                 self.step_count, s)
+
+    # ---- torch.optim.Adam-compatible checkpoint format ----
+    def state_dict(self):
+        state = {}
+        idx = 0
+        for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
+            for p, off in zip(f.params, f.offsets):
+                n = p.numel()
+                state[idx] = {"step": torch.tensor(float(self.step_count)),
+                              "exp_avg": m[off:off + n].view_as(p).clone(),
+                              "exp_avg_sq": v[off:off + n].view_as(p).clone()}
+                idx += 1
+        group = {k: v for k, v in self.param_groups[0].items() if k != "params"}
+        group["params"] = list(range(idx))
+        return {"state": state, "param_groups": [group]}
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        st = sd["state"]
+        idx = 0
+        steps = []
+        for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
+            for p, off in zip(f.params, f.offsets):
+                n = p.numel()
+                if idx in st:
+                    m[off:off + n].copy_(st[idx]["exp_avg"].reshape(-1))
+                    v[off:off + n].copy_(st[idx]["exp_avg_sq"].reshape(-1))
+                    steps.append(int(float(st[idx]["step"])))
+                idx += 1
+        if steps:
+            self.step_count = max(steps)
+        g = sd["param_groups"][0]
+        self.param_groups[0]["lr"] = g.get("lr", self.lr)
+        self.lr = float(self.param_groups[0]["lr"])
+        self.betas = tuple(g.get("betas", self.betas))
+        self.eps = g.get("eps", self.eps)
+        self.weight_decay = g.get("weight_decay", self.weight_decay)
+
+
+def _unused():  # keep ctypes imported for type checkers of call sites
+    return ctypes
