@@ -44,12 +44,20 @@ const char* vae2_last_error(void);
  * Workspace = 2 * rows * cout floats.                                         */
 int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout);
 
-/* y = conv2d(x, w, stride, pad) (+ bias) (+ beta*y), optional per-channel BN
- * partial sums of the result in `stats` (layout [2][rows][cout]).
+/* Conv weights are consumed in a packed layout (zero-padded, K = (tap, 4-channel
+ * quad) ordered): mode 0 for vae2_conv2d_fwd  = [round_up(Cout,64)][k*k][round_up(Cin,4)],
+ * mode 1 for vae2_conv2d_bwd_data = [round_up(Cin,64)][k*k][round_up(Cout,4)].
+ * Size in floats / packing from the reference [Cout][Cin][k][k] layout:          */
+int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode);
+int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k,
+                            int mode, float* out, void* stream);
+
+/* y = conv2d(x, w, stride, pad) (+ bias) (+ beta*y) with w packed (mode 0),
+ * optional per-channel BN partial sums of the result in `stats` ([2][rows][cout]).
  * Replaces nn.Conv2d.forward: conv3x3 enc_hrnet.py:27-30, Bottleneck 1x1
  * :70-76, downsample :411-415, fuse :188-217, transitions :381-403, heads
  * :323-370/:598-750, z head :1026-1039.                                       */
-int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* w,
+int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
                     const float* bias, float* y, const vae2_act* yd, int k,
                     int stride, int pad, float beta, float* stats,
                     void* stream);
@@ -59,9 +67,9 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* w,
 int vae2_conv2d_fwd_kernel_name(const vae2_act* yd, int64_t cout, char* buf,
                                 int64_t len);
 
-/* dx = conv2d_transpose(dy, w) (+ beta*dx): gradient of vae2_conv2d_fwd w.r.t.
- * its input (autograd's convolution_backward, input half).                    */
-int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* w,
+/* dx = conv2d_transpose(dy, w) (+ beta*dx) with w packed (mode 1): gradient of
+ * vae2_conv2d_fwd w.r.t. its input (autograd's convolution_backward, input half). */
+int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
                          float* dx, const vae2_act* dxd, int k, int stride,
                          int pad, float beta, void* stream);
 

@@ -1,180 +1,186 @@
 // Convolutions of the HRNet stacks as implicit GEMMs on the fp32 matrix cores
 // (v_mfma_f32_16x16x4_f32: exact fp32 FMA chains, 64 FLOP/clk/SIMD on gfx950).
 //
-//   forward     Y[m][n]  = sum_k A[m][k] * B[k][n]
-//               m = output pixel, n = Cout, k = (tap, Cin); A = im2col(X) gathered
-//               on the fly from NHWC, B = W[Cout][Cin][kh][kw] read in place.
-//   bwd data    same kernel: m = input pixel (one stride-parity class per launch),
-//               n = Cin, k = (valid tap, Cout), A = dY gathered, B = W^T.
-//   bwd weight  dW[co][(tap,ci)] = sum_p dY[p][co] * X[src(p,tap)][ci], split over
-//               pixels (split-K) into fp32 slabs, then a fixed-order reduction
+//   forward     Y[m][n] = sum_k A[m][k] * B[k][n]
+//               m = output pixel, n = Cout, k = (tap, Cin4); A = im2col(X) gathered
+//               from NHWC on the fly, B = weights packed [Npad][k*k][Cin4].
+//   bwd data    same kernel: m = input pixel of one stride-parity class per launch,
+//               n = Cin, k = (valid tap, Cout4), A = dY gathered, B = weights packed
+//               [Cin_pad][k*k][Cout4] (the transposed conv).
+//   bwd weight  dW[co][(tap, ci)] = sum_p dY[p][co] * X[src(p, tap)][ci], split over
+//               pixels into fp32 slabs (one per wave), then a fixed-order reduction
 //               into the [Cout][Cin][kh][kw] gradient (deterministic).
 //
-// Replaces nn.Conv2d forward/backward for every conv of enc_hrnet.py (see
-// include/vae2_hip.h for the call sites).
+// Fragment-direct loads: Cin is padded to a multiple of 4 (Cin4) inside K, and in
+// each 16-deep K chunk lane group g = lane>>4 owns the 4 consecutive k = 4g..4g+3,
+// i.e. 4 consecutive channels of ONE tap.  MFMA k-step s uses k = 4g+s for both
+// operands (a permutation of the reduction order the sum does not see).  So a
+// lane's A fragment for 4 k-steps is one 16-byte load of an NHWC pixel and its B
+// fragment one 16-byte load of the packed weights: no LDS staging, no barriers in
+// the main loop; fragments are double-buffered in registers.
 //
-// K ordering trick: within each 16-deep K chunk, lane group g = lane>>4 owns
-// k = 4g..4g+3, and MFMA k-step s uses k = 4g+s for both operands.  The A and B
-// fragments of all four k-steps then come from ONE 16-byte LDS read per lane
-// (layout [g][row][4], conflict-free for ds_read_b128) — a permutation of the
-// reduction order that the sum does not see.
+// Replaces nn.Conv2d forward/backward for every conv of enc_hrnet.py (call sites
+// in include/vae2_hip.h).
 #include "common.h"
 
 namespace vae2 {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// ------------------------------------------------- range-checked loads ----
+// A raw buffer load whose byte offset is >= the descriptor's num_records returns 0.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  uint64_t b = (uint64_t)base;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* pb = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// ------------------------------------------------------------ weight pack ----
+// mode 0: out[n][t][c4] = w[n][c][t]         n < round_up(cout,64), c4 < round_up(cin,4)
+// mode 1: out[n][t][c4] = w[c][n][t]         n < round_up(cin,64),  c4 < round_up(cout,4)
+// (rows padded to 64 = the widest N tile, so B loads never need a bounds check)
+__global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int kk,
+                                   int mode, float* __restrict__ out) {
+  const int rows = mode == 0 ? (cout + 63) / 64 * 64 : (cin + 63) / 64 * 64;
+  const int cols4 = mode == 0 ? (cin + 3) / 4 * 4 : (cout + 3) / 4 * 4;
+  const int total = rows * kk * cols4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int n = i / (kk * cols4);
+    int rem = i - n * kk * cols4;
+    int t = rem / cols4;
+    int c = rem - t * cols4;
+    float v = 0.f;
+    if (mode == 0) {
+      if (n < cout && c < cin) v = w[((int64_t)n * cin + c) * kk + t];
+    } else {
+      if (n < cin && c < cout) v = w[((int64_t)c * cin + n) * kk + t];
+    }
+    out[i] = v;
+  }
+}
+
+// ------------------------------------------------------------ igemm ----
 struct IGemm {
-  // A operand: activation gathered from NHWC
-  const float* a;
-  int64_t a_ps;
-  int a_c, a_h, a_w;
-  // iteration grid: M = g_n * g_h * g_w rows
-  int g_n, g_h, g_w;
-  int a_step;  // A source row = g*a_step + d(tap)
-  // taps: t = th*ntw + tw;  d = d0 + th*ds;  weight tap (kh0 + th*khs, kw0 + tw*kws)
-  int nth, ntw;
+  const float* a;  // gathered activation (NHWC)
+  int a_ps, a_c, a_c4, a_h, a_w;
+  int g_n, g_h, g_w;  // iteration grid, M = g_n*g_h*g_w
+  int a_step;         // A source row = g*a_step + d(tap)
+  int nth, ntw;       // taps: t = th*ntw + tw
   int dh0, dhs, dw0, dws;
-  int kh0, khs, kw0, kws, kw_size;
-  // B operand: B[n][(t, c)] = w[n*w_sn + c*w_sc + kh*kw_size + kw]
-  const float* w;
-  int64_t w_sn, w_sc;
-  int n;
+  int kh0, khs, kw0, kws, ksz;  // weight tap (kh0 + th*khs, kw0 + tw*kws) of a ksz x ksz kernel
+  const float* w;               // packed [Npad][ksz*ksz][a_c4]
+  uint32_t a_bytes, w_bytes;    // buffer extents for the range-checked loads
+  int n;                        // GEMM N (real)
   const float* bias;
-  // output: row (gi*y_step + y_offh), col (gj*y_step + y_offw)
   float* y;
-  int64_t y_ps;
-  int y_h, y_w, y_step, y_offh, y_offw;
+  int y_ps, y_h, y_w, y_step, y_offh, y_offw;
   float beta;
   float* stats;  // [2][gridDim.x][n] or null
+  FastDiv hw_div, w_div;  // divide by g_h*g_w, g_w
 };
 
-constexpr int BK = 16;
-
-// ROLE only separates forward (0) and data-gradient (1) launches in profiles.
-template <int TM, int TN, int ROLE>
+template <int TM, int TN, bool VEC, int ROLE>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
-  constexpr int BM = 64 * TM;
   constexpr int BN = 16 * TN;
-  constexpr int A_F = 4 * BM * 4;  // floats per A buffer: [4 groups][BM][4]
-  constexpr int B_F = 4 * BN * 4;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (A_F + B_F)];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  __shared__ float red[4][2][BN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int M = p.g_n * p.g_h * p.g_w;
+  const int mw = (blockIdx.x * 4 + wave) * (16 * TM);
   const int n0 = blockIdx.y * BN;
-  const int ntaps = p.nth * p.ntw;
-  const int K = ntaps * p.a_c;
-  const int nchunks = (K + BK - 1) / BK;
+  const int kk4 = p.ksz * p.ksz * p.a_c4;
 
-  // ---- per-thread gather rows (A) ----
-  const int q = tid & 3;          // k quad owned by this thread in a chunk
-  const int rbase = tid >> 2;     // 0..63
-  int64_t a_img[TM];
-  int a_i[TM], a_j[TM];
-  bool a_ok[TM];
+  // this lane's A rows: m = mw + i*16 + r
+  int rpix[TM], ri[TM], rj[TM];
+  bool rok[TM];
 #pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    int64_t m = m0 + rbase + 64 * j;
-    a_ok[j] = m < M;
-    int64_t mm = a_ok[j] ? m : 0;
-    int64_t hw = (int64_t)p.g_h * p.g_w;
-    int64_t gn = mm / hw;
-    int64_t rem = mm - gn * hw;
-    int gi = (int)(rem / p.g_w);
-    int gj = (int)(rem - (int64_t)gi * p.g_w);
-    a_img[j] = gn * p.a_h;
-    a_i[j] = gi * p.a_step;
-    a_j[j] = gj * p.a_step;
+  for (int i = 0; i < TM; ++i) {
+    int m = mw + i * 16 + r;
+    rok[i] = m < M;
+    int mm = rok[i] ? m : 0;
+    int gn = (int)p.hw_div.div((uint32_t)mm);
+    int rem = mm - gn * p.g_h * p.g_w;
+    int gi = (int)p.w_div.div((uint32_t)rem);
+    int gj = rem - gi * p.g_w;
+    ri[i] = gi * p.a_step;
+    rj[i] = gj * p.a_step;
+    rpix[i] = (gn * p.a_h + ri[i]) * p.a_w + rj[i];
   }
-  // B rows owned by this thread
-  constexpr int BROWS = (BN + 63) / 64;
-  // (tap, channel) of k = chunk*16 + 4q
-  int tb = 0, cb = 4 * q;
-  while (cb >= p.a_c) { cb -= p.a_c; ++tb; }
+  // Buffer resources (wave-uniform): out-of-range offsets load 0, so padding taps,
+  // rows past M and the K tail need no branches.
+  const __amdgpu_buffer_rsrc_t arsrc = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(p.w, p.w_bytes);
+  uint32_t wrow[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) wrow[j] = (uint32_t)((n0 + j * 16 + r) * kk4) * 4u;
 
-  float ra[TM][4];
-  float rb[BROWS][4];
+  const int ntaps = p.nth * p.ntw;
+  const int K = ntaps * p.a_c4;
+  const int nchunks = (K + 15) >> 4;
+  int tt = 0, c0 = 4 * g;
+  while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
+  const bool cpad = (p.a_c & 3) != 0;
 
-  auto load_chunk = [&](int chunk_t, int chunk_c) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int t = chunk_t, c = chunk_c + e;
-      while (c >= p.a_c) { c -= p.a_c; ++t; }
-      bool tv = t < ntaps;
-      int th = tv ? t / p.ntw : 0;
-      int tw = tv ? t - th * p.ntw : 0;
-      int dh = p.dh0 + th * p.dhs;
-      int dw = p.dw0 + tw * p.dws;
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        int ih = a_i[j] + dh, iw = a_j[j] + dw;
-        bool ok = tv && a_ok[j] && ih >= 0 && ih < p.a_h && iw >= 0 && iw < p.a_w;
-        float v = 0.f;
-        if (ok) v = p.a[((a_img[j] + ih) * p.a_w + iw) * p.a_ps + c];
-        ra[j][e] = v;
-      }
-      int kh = p.kh0 + th * p.khs, kw = p.kw0 + tw * p.kws;
-      int64_t toff = (int64_t)kh * p.kw_size + kw;
-#pragma unroll
-      for (int j = 0; j < BROWS; ++j) {
-        int nr = rbase + 64 * j;
-        float v = 0.f;
-        if (tv && nr < BN && n0 + nr < p.n)
-          v = p.w[(int64_t)(n0 + nr) * p.w_sn + (int64_t)c * p.w_sc + toff];
-        rb[j][e] = v;
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-    float* As = smem + buf * (A_F + B_F);
-    float* Bs = As + A_F;
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      f4 v = {ra[j][0], ra[j][1], ra[j][2], ra[j][3]};
-      *reinterpret_cast<f4*>(As + (q * BM + rbase + 64 * j) * 4) = v;
-    }
-#pragma unroll
-    for (int j = 0; j < BROWS; ++j) {
-      int nr = rbase + 64 * j;
-      if (nr < BN) {
-        f4 v = {rb[j][0], rb[j][1], rb[j][2], rb[j][3]};
-        *reinterpret_cast<f4*>(Bs + (q * BN + nr) * 4) = v;
-      }
-    }
-  };
-
+  f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
   f4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  const int g = lane >> 4, r = lane & 15;
-  const int wm0 = wave * 16 * TM;
-
-  if (nchunks > 0) load_chunk(tb, cb);
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int buf = ch & 1;
-    store_chunk(buf);
-    __syncthreads();
-    if (ch + 1 < nchunks) {
-      cb += BK;
-      while (cb >= p.a_c) { cb -= p.a_c; ++tb; }
-      load_chunk(tb, cb);
+  auto load = [&](f4* fa, f4* fb) {
+    const bool tv = tt < ntaps;
+    const int tc = tv ? tt : 0;
+    const int th = tc / p.ntw;
+    const int tw = tc - th * p.ntw;
+    const int dh = p.dh0 + th * p.dhs, dw = p.dw0 + tw * p.dws;
+    const int tlin = (p.kh0 + th * p.khs) * p.ksz + (p.kw0 + tw * p.kws);
+    const uint32_t woff = tv ? (uint32_t)(tlin * p.a_c4 + c0) * 4u : kOOB;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
+    const int doff = dh * p.a_w + dw;
+    const bool m1 = c0 + 1 < p.a_c, m2 = c0 + 2 < p.a_c, m3 = c0 + 3 < p.a_c;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ih = ri[i] + dh, iw = rj[i] + dw;
+      const bool ok = tv && rok[i] && (unsigned)ih < (unsigned)p.a_h &&
+                      (unsigned)iw < (unsigned)p.a_w;
+      const uint32_t off = ok ? (uint32_t)((rpix[i] + doff) * p.a_ps + c0) * 4u : kOOB;
+      f4 v;
+      if (VEC) {
+        v = load4(arsrc, off);
+        if (cpad) {
+          v[1] = m1 ? v[1] : 0.f;
+          v[2] = m2 ? v[2] : 0.f;
+          v[3] = m3 ? v[3] : 0.f;
+        }
+      } else {
+        v[0] = load1(arsrc, off);
+        v[1] = load1(arsrc, m1 ? off + 4u : kOOB);
+        v[2] = load1(arsrc, m2 ? off + 8u : kOOB);
+        v[3] = load1(arsrc, m3 ? off + 12u : kOOB);
+      }
+      fa[i] = v;
     }
-    const float* As = smem + buf * (A_F + B_F);
-    const float* Bs = As + A_F;
-    f4 fa[TM], fb[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-      fa[i] = *reinterpret_cast<const f4*>(As + (g * BM + wm0 + i * 16 + r) * 4);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      fb[j] = *reinterpret_cast<const f4*>(Bs + (g * BN + j * 16 + r) * 4);
+    c0 += 16;
+    while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
+  };
+  auto mma = [&](const f4* fa, const f4* fb) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -182,10 +188,20 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  // Chunk pairs; the (possibly) extra odd chunk loads zeros (tt >= ntaps).
+  if (mw < M) {
+    load(fa0, fb0);
+    for (int ch = 0; ch < nchunks; ch += 2) {
+      load(fa1, fb1);
+      mma(fa0, fb0);
+      load(fa0, fb0);
+      mma(fa1, fb1);
+    }
   }
 
   // ---- epilogue ----
-  const int64_t hw = (int64_t)p.g_h * p.g_w;
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
@@ -193,18 +209,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      int64_t m = m0 + wm0 + i * 16 + g * 4 + e;
+      const int m = mw + i * 16 + g * 4 + e;
       if (m >= M) continue;
-      int64_t gn = m / hw;
-      int64_t rem = m - gn * hw;
-      int gi = (int)(rem / p.g_w);
-      int gj = (int)(rem - (int64_t)gi * p.g_w);
-      int64_t oy = (int64_t)gi * p.y_step + p.y_offh;
-      int64_t ox = (int64_t)gj * p.y_step + p.y_offw;
+      const int gn = (int)p.hw_div.div((uint32_t)m);
+      const int rem = m - gn * p.g_h * p.g_w;
+      const int gi = (int)p.w_div.div((uint32_t)rem);
+      const int gj = rem - gi * p.g_w;
+      const int oy = gi * p.y_step + p.y_offh;
+      const int ox = gj * p.y_step + p.y_offw;
       float* yrow = p.y + ((gn * p.y_h + oy) * p.y_w + ox) * p.y_ps;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        int n = n0 + j * 16 + r;
+        const int n = n0 + j * 16 + r;
         if (n >= p.n) continue;
         float v = acc[i][j][e];
         if (p.bias) v += p.bias[n];
@@ -216,7 +232,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
     }
   }
   if (p.stats) {
-    // reduce over the 4 row groups of the wave (lanes r, r+16, r+32, r+48)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       csum[j] += __shfl_xor(csum[j], 16, 64);
@@ -224,26 +239,20 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
       csq[j] += __shfl_xor(csq[j], 16, 64);
       csq[j] += __shfl_xor(csq[j], 32, 64);
     }
-    __syncthreads();  // done with operand buffers: reuse smem
-    float* red = smem;  // [4 waves][2][BN]
     if (g == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        red[(wave * 2 + 0) * BN + j * 16 + r] = csum[j];
-        red[(wave * 2 + 1) * BN + j * 16 + r] = csq[j];
+        red[wave][0][j * 16 + r] = csum[j];
+        red[wave][1][j * 16 + r] = csq[j];
       }
     }
     __syncthreads();
-    const int64_t rows = gridDim.x;
-    for (int c = tid; c < BN; c += 256) {
+    const int rows = gridDim.x;
+    for (int c = threadIdx.x; c < BN; c += 256) {
       if (n0 + c >= p.n) continue;
-      float s = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        s += red[(w * 2 + 0) * BN + c];
-        s2 += red[(w * 2 + 1) * BN + c];
-      }
-      p.stats[(int64_t)blockIdx.x * p.n + n0 + c] = s;
+      float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+      p.stats[blockIdx.x * p.n + n0 + c] = s;
       p.stats[(rows + blockIdx.x) * p.n + n0 + c] = s2;
     }
   }
@@ -257,38 +266,53 @@ struct Tile {
 static Tile pick_tile(int64_t M, int N) {
   Tile t;
   int tiles = (N + 15) / 16;
-  if (tiles <= 9) {
+  if (tiles <= 4) {
     t.tn = tiles;
     t.nblk = 1;
   } else {
-    t.nblk = (tiles + 7) / 8;
+    t.nblk = (tiles + 3) / 4;
     t.tn = (tiles + t.nblk - 1) / t.nblk;
   }
-  t.tm = (M >= 128 * 256) ? 2 : 1;
+  // 4 waves per block, 16*TM rows per wave; large TM once there are enough rows
+  t.tm = (M >= 64 * 4 * 256) ? 4 : (M >= 32 * 4 * 128 ? 2 : 1);
   return t;
 }
 
-template <int TM, int ROLE>
+template <int TM, bool VEC, int ROLE>
 static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((igemm_kernel<TM, T, ROLE>), grid, dim3(256), 0, s, p); break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
+  case T: hipLaunchKernelGGL((igemm_kernel<TM, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
 }
 
-static int launch_igemm(const IGemm& p, int role, hipStream_t s, const char* fn) {
+template <bool VEC, int ROLE>
+static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
+  if (t.tm == 4) launch_tn<4, VEC, ROLE>(p, t.tn, grid, s);
+  else if (t.tm == 2) launch_tn<2, VEC, ROLE>(p, t.tn, grid, s);
+  else launch_tn<1, VEC, ROLE>(p, t.tn, grid, s);
+}
+
+static bool vec_ok(const float* a, int ps) {
+  return ((uintptr_t)a % 16 == 0) && (ps % 4 == 0);
+}
+
+static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn) {
   int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
   if (M == 0) return 0;
   Tile t = pick_tile(M, p.n);
+  p.hw_div = FastDiv((uint32_t)(p.g_h * p.g_w));
+  p.w_div = FastDiv((uint32_t)p.g_w);
   dim3 grid((unsigned)ceil_div(M, 64 * t.tm), (unsigned)t.nblk);
+  bool vec = vec_ok(p.a, p.a_ps);
   if (role == 0) {
-    if (t.tm == 2) launch_tn<2, 0>(p, t.tn, grid, s);
-    else launch_tn<1, 0>(p, t.tn, grid, s);
+    if (vec) launch_tm<true, 0>(p, t, grid, s);
+    else launch_tm<false, 0>(p, t, grid, s);
   } else {
-    if (t.tm == 2) launch_tn<2, 1>(p, t.tn, grid, s);
-    else launch_tn<1, 1>(p, t.tn, grid, s);
+    if (vec) launch_tm<true, 1>(p, t, grid, s);
+    else launch_tm<false, 1>(p, t, grid, s);
   }
   return check_launch(fn);
 }
@@ -299,128 +323,77 @@ static int64_t igemm_rows(int64_t M, int N) {
 }
 
 // ------------------------------------------------------------ wgrad ----
+// One wave per workgroup.  Tile: 16*TM output channels x 16*TN (tap, cin4) columns,
+// over a pixel range; partial tile -> part[split][cout][ncol4] (ncol4 = k*k*cin4).
 struct WGrad {
-  const float* x;  // B operand source (NHWC)
-  int64_t x_ps;
-  int cin, x_h, x_w;
-  const float* dy;  // A operand source (NHWC)
-  int64_t dy_ps;
-  int cout, o_n, o_h, o_w;
+  const float* x;
+  int x_ps, cin, cin4, x_h, x_w;
+  const float* dy;
+  int dy_ps, cout, o_n, o_h, o_w;
   int k, stride, pad;
-  int64_t P;          // o_n*o_h*o_w
-  int64_t px_split;   // pixels per split (multiple of 16)
-  float* part;        // [split][cout][ncol], ncol = k*k*cin
+  int P, px_split;
+  float* part;
+  FastDiv ohw_div, ow_div, cin4_div;
 };
 
-// Block: 4 waves along the (tap, cin) columns; wave tile 16*TM rows (cout) x 16*TN cols.
 template <int TM, int TN>
-__global__ __launch_bounds__(256) void wgrad_kernel(WGrad p) {
-  constexpr int BM = 16 * TM;       // cout rows per block
-  constexpr int BN = 64 * TN;       // (tap, cin) columns per block
-  constexpr int A_F = 4 * BM * 4;   // [g][BM][4]
-  constexpr int B_F = 4 * BN * 4;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (A_F + B_F)];
+__global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, r = lane & 15;
+  const int ncol4 = p.k * p.k * p.cin4;
+  const int co0 = blockIdx.y * 16 * TM;
+  const int col0 = blockIdx.x * 16 * TN;
+  const int pbeg = blockIdx.z * p.px_split;
+  const int pend = min(pbeg + p.px_split, p.P);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ncol = p.k * p.k * p.cin;
-  const int co0 = blockIdx.y * BM;
-  const int col0 = blockIdx.x * BN;
-  const int64_t pbeg = (int64_t)blockIdx.z * p.px_split;
-  int64_t pend = pbeg + p.px_split;
-  if (pend > p.P) pend = p.P;
-  const int nchunks = (int)((pend - pbeg + BK - 1) / BK);
-
-  // Loading: A' tile BM x 16 pixels; B' tile BN x 16 pixels.
-  // thread -> (quad q of pixels, row) : q = tid & 3, rows tid>>2 (+64j)
-  const int q = tid & 3, rbase = tid >> 2;
-  constexpr int AROWS = (BM + 63) / 64;
-  constexpr int BROWS = BN / 64;  // == TN
-  // B' column decomposition (tap, ci) per owned row
-  int b_kh[BROWS], b_kw[BROWS], b_ci[BROWS];
-  bool b_ok[BROWS];
+  int aco[TM];
+  bool aok[TM];
 #pragma unroll
-  for (int j = 0; j < BROWS; ++j) {
-    int col = col0 + rbase + 64 * j;
-    b_ok[j] = col < ncol;
-    int cc = b_ok[j] ? col : 0;
-    int t = cc / p.cin;
-    b_ci[j] = cc - t * p.cin;
-    b_kh[j] = t / p.k;
-    b_kw[j] = t - b_kh[j] * p.k;
+  for (int i = 0; i < TM; ++i) {
+    aco[i] = co0 + i * 16 + r;
+    aok[i] = aco[i] < p.cout;
   }
-  float ra[AROWS][4], rb[BROWS][4];
-  const int64_t ohw = (int64_t)p.o_h * p.o_w;
-
-  auto load_chunk = [&](int64_t pc) {
+  int bkh[TN], bkw[TN], bci[TN];
+  bool bok[TN];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int64_t pix = pc + 4 * q + e;
-      bool pv = pix < pend;
-      int64_t pp = pv ? pix : 0;
-      int64_t n = pp / ohw;
-      int64_t rem = pp - n * ohw;
-      int oh = (int)(rem / p.o_w);
-      int ow = (int)(rem - (int64_t)oh * p.o_w);
-      const float* dyrow = p.dy + pp * p.dy_ps;
-#pragma unroll
-      for (int j = 0; j < AROWS; ++j) {
-        int co = co0 + rbase + 64 * j;
-        float v = 0.f;
-        if (pv && rbase + 64 * j < BM && co < p.cout) v = dyrow[co];
-        ra[j][e] = v;
-      }
-#pragma unroll
-      for (int j = 0; j < BROWS; ++j) {
-        int ih = oh * p.stride - p.pad + b_kh[j];
-        int iw = ow * p.stride - p.pad + b_kw[j];
-        float v = 0.f;
-        if (pv && b_ok[j] && ih >= 0 && ih < p.x_h && iw >= 0 && iw < p.x_w)
-          v = p.x[((n * p.x_h + ih) * p.x_w + iw) * p.x_ps + b_ci[j]];
-        rb[j][e] = v;
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-    float* As = smem + buf * (A_F + B_F);
-    float* Bs = As + A_F;
-#pragma unroll
-    for (int j = 0; j < AROWS; ++j) {
-      int rr = rbase + 64 * j;
-      if (rr < BM) {
-        f4 v = {ra[j][0], ra[j][1], ra[j][2], ra[j][3]};
-        *reinterpret_cast<f4*>(As + (q * BM + rr) * 4) = v;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < BROWS; ++j) {
-      f4 v = {rb[j][0], rb[j][1], rb[j][2], rb[j][3]};
-      *reinterpret_cast<f4*>(Bs + (q * BN + rbase + 64 * j) * 4) = v;
-    }
-  };
-
+  for (int j = 0; j < TN; ++j) {
+    int col = col0 + j * 16 + r;
+    int t = (int)p.cin4_div.div((uint32_t)col);
+    bci[j] = col - t * p.cin4;
+    bkh[j] = t / p.k;
+    bkw[j] = t - bkh[j] * p.k;
+    bok[j] = col < ncol4 && bci[j] < p.cin;
+  }
   f4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  const int g = lane >> 4, r = lane & 15;
-  const int wn0 = wave * 16 * TN;
 
-  if (nchunks > 0) load_chunk(pbeg);
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int buf = ch & 1;
-    store_chunk(buf);
-    __syncthreads();
-    if (ch + 1 < nchunks) load_chunk(pbeg + (int64_t)(ch + 1) * BK);
-    const float* As = smem + buf * (A_F + B_F);
-    const float* Bs = As + A_F;
+  const int ohw = p.o_h * p.o_w;
+  for (int pc = pbeg; pc < pend; pc += 16) {
     f4 fa[TM], fb[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-      fa[i] = *reinterpret_cast<const f4*>(As + (g * BM + i * 16 + r) * 4);
+    for (int s = 0; s < 4; ++s) {
+      const int pix = pc + 4 * g + s;
+      const bool pv = pix < pend;
+      const int pp = pv ? pix : pbeg;
+      const int n = (int)p.ohw_div.div((uint32_t)pp);
+      const int rem = pp - n * ohw;
+      const int oh = (int)p.ow_div.div((uint32_t)rem);
+      const int ow = rem - oh * p.o_w;
+      const float* dyrow = p.dy + pp * p.dy_ps;
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      fb[j] = *reinterpret_cast<const f4*>(Bs + (g * BN + wn0 + j * 16 + r) * 4);
+      for (int i = 0; i < TM; ++i) fa[i][s] = (pv && aok[i]) ? dyrow[aco[i]] : 0.f;
+      const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
+      const int xbase = n * p.x_h;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int ih = ih0 + bkh[j], iw = iw0 + bkw[j];
+        const bool ok = pv && bok[j] && ih >= 0 && ih < p.x_h && iw >= 0 && iw < p.x_w;
+        fb[j][s] = ok ? p.x[((xbase + ih) * p.x_w + iw) * p.x_ps + bci[j]] : 0.f;
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -430,75 +403,77 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGrad p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   }
 
-  float* out = p.part + (int64_t)blockIdx.z * p.cout * ncol;
+  float* out = p.part + (int64_t)blockIdx.z * p.cout * ncol4;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      int co = co0 + i * 16 + g * 4 + e;
+      const int co = co0 + i * 16 + g * 4 + e;
       if (co >= p.cout) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        int col = col0 + wn0 + j * 16 + r;
-        if (col < ncol) out[(int64_t)co * ncol + col] = acc[i][j][e];
+        const int col = col0 + j * 16 + r;
+        if (col < ncol4) out[(int64_t)co * ncol4 + col] = acc[i][j][e];
       }
     }
 }
 
-// dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin + ci]
-__global__ void wgrad_reduce_kernel(const float* part, int64_t splits, int cout,
-                                    int cin, int k, float* dw, int accumulate) {
-  const int ncol = k * k * cin;
-  const int64_t total = (int64_t)cout * ncol;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int co = (int)(idx / ncol);
-    int col = (int)(idx - (int64_t)co * ncol);
+// dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin4 + ci]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int cout,
+                                    int cin, int cin4, int k, float* __restrict__ dw,
+                                    int accumulate) {
+  const int kk = k * k;
+  const int ncol4 = kk * cin4;
+  const int total = cout * cin * kk;  // over the OIHW gradient
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int co = idx / (cin * kk);
+    const int rem = idx - co * cin * kk;
+    const int ci = rem / kk;
+    const int t = rem - ci * kk;
+    const int64_t src = (int64_t)co * ncol4 + t * cin4 + ci;
+    const int64_t stride = (int64_t)cout * ncol4;
     float s = 0.f;
-    for (int64_t sp = 0; sp < splits; ++sp) s += part[sp * total + idx];
-    int t = col / cin;
-    int ci = col - t * cin;
-    int64_t o = ((int64_t)co * cin + ci) * (k * k) + t;
-    dw[o] = accumulate ? dw[o] + s : s;
+    for (int sp = 0; sp < splits; ++sp) s += part[sp * stride + src];
+    dw[idx] = accumulate ? dw[idx] + s : s;
   }
 }
 
 struct WTile {
-  int tm, tn;
-  int64_t splits, px_split;
-  int gx, gy;
+  int tm, tn, gx, gy, splits, px_split;
 };
 
-static WTile pick_wtile(int64_t P, int cout, int ncol) {
+static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   WTile t;
   int mt = (cout + 15) / 16;
   t.tm = mt <= 4 ? mt : 4;
-  int ct = (ncol + 63) / 64;  // 64-column units
-  t.tn = ct <= 2 ? ct : 2;
   t.gy = (int)ceil_div(cout, 16 * t.tm);
-  t.gx = (int)ceil_div(ncol, 64 * t.tn);
+  int ct = (ncol4 + 15) / 16;
+  t.tn = ct <= 4 ? ct : 4;
+  t.gx = (int)ceil_div(ncol4, 16 * t.tn);
   int64_t tiles = (int64_t)t.gx * t.gy;
-  // aim for ~2048 workgroups, at least 256 pixels (16 chunks) per split
-  int64_t want = ceil_div(2048, tiles);
-  int64_t maxs = ceil_div(P, 256);
+  // ~4096 waves in flight, at least 512 pixels (32 chunks) per wave
+  int64_t want = ceil_div(4096, tiles);
+  int64_t maxs = ceil_div(P, 512);
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;
-  t.px_split = ceil_div(ceil_div(P, s), BK) * BK;
-  t.splits = ceil_div(P, t.px_split);
+  t.px_split = (int)(ceil_div(ceil_div(P, s), 16) * 16);
+  t.splits = (int)ceil_div(P, t.px_split);
   return t;
 }
 
 template <int TM>
 static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
-  if (tn == 1)
-    hipLaunchKernelGGL((wgrad_kernel<TM, 1>), grid, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<TM, 2>), grid, dim3(256), 0, s, p);
+  switch (tn) {
+    case 1: hipLaunchKernelGGL((wgrad_kernel<TM, 1>), grid, dim3(64), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((wgrad_kernel<TM, 2>), grid, dim3(64), 0, s, p); break;
+    case 3: hipLaunchKernelGGL((wgrad_kernel<TM, 3>), grid, dim3(64), 0, s, p); break;
+    default: hipLaunchKernelGGL((wgrad_kernel<TM, 4>), grid, dim3(64), 0, s, p); break;
+  }
 }
 
 // ------------------------------------------------------------- checks ----
-static bool conv_shapes_ok(const vae2_act* xd, const vae2_act* yd, int k,
-                           int stride, int pad) {
+static bool conv_shapes_ok(const vae2_act* xd, const vae2_act* yd, int k, int stride, int pad) {
   if (!act_ok(xd) || !act_ok(yd)) return false;
   if (xd->n != yd->n) return false;
   if (k < 1 || stride < 1 || pad < 0) return false;
@@ -507,11 +482,42 @@ static bool conv_shapes_ok(const vae2_act* xd, const vae2_act* yd, int k,
   return oh == yd->h && ow == yd->w;
 }
 
+static bool fits32(const vae2_act* d) {
+  return d->n * d->h * d->w * d->ps < (int64_t(1) << 29);  // byte offsets < 2^31
+}
+
+// Bytes spanned by an activation view, for buffer descriptors.  With 16-byte
+// aligned pixels (ps % 4 == 0) the last pixel's final 4-channel quad is included
+// (it lies inside the pixel stride), so a whole-access range check never drops
+// real channels of the last quad.
+static uint32_t act_bytes(const vae2_act* d) {
+  int64_t tail = (d->ps % 4 == 0) ? ((d->c + 3) / 4 * 4) : d->c;
+  int64_t last = ((d->n * d->h * d->w) - 1) * d->ps + tail;
+  return (uint32_t)(last * 4);
+}
+
 }  // namespace vae2
 
 using namespace vae2;
 
 extern "C" {
+
+int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode) {
+  int rows = mode == 0 ? round_up((int)cout, 64) : round_up((int)cin, 64);
+  int cols4 = mode == 0 ? round_up((int)cin, 4) : round_up((int)cout, 4);
+  return (int64_t)rows * k * k * cols4;
+}
+
+int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k, int mode,
+                            float* out, void* stream) {
+  const char* fn = "vae2_conv2d_pack_weight";
+  VAE2_REQUIRE(w && out && cout > 0 && cin > 0 && k > 0 && (mode == 0 || mode == 1), fn,
+               "bad arguments");
+  int64_t total = vae2_conv2d_packed_size(cout, cin, k, mode);
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0,
+                     as_stream(stream), w, (int)cout, (int)cin, k * k, mode, out);
+  return check_launch(fn);
+}
 
 int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout) {
   return igemm_rows(act_pixels(yd), (int)cout);
@@ -520,65 +526,70 @@ int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout) {
 int vae2_conv2d_fwd_kernel_name(const vae2_act* yd, int64_t cout, char* buf, int64_t len) {
   if (!yd || !buf || len <= 0) return -22;
   Tile t = pick_tile(act_pixels(yd), (int)cout);
-  snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, 0>", t.tm, t.tn);
+  snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0>", t.tm, t.tn);
   return 0;
 }
 
-int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* w,
+int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
                     const float* bias, float* y, const vae2_act* yd, int k,
                     int stride, int pad, float beta, float* stats,
                     void* stream) {
   const char* fn = "vae2_conv2d_fwd";
-  VAE2_REQUIRE(x && w && y, fn, "null pointer");
+  VAE2_REQUIRE(x && wp && y, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(xd, yd, k, stride, pad), fn, "inconsistent conv shapes");
+  VAE2_REQUIRE(fits32(xd) && fits32(yd), fn, "tensor too large for 32-bit indexing");
   IGemm p{};
-  p.a = x; p.a_ps = xd->ps; p.a_c = (int)xd->c; p.a_h = (int)xd->h; p.a_w = (int)xd->w;
+  p.a = x; p.a_ps = (int)xd->ps; p.a_c = (int)xd->c; p.a_c4 = round_up((int)xd->c, 4);
+  p.a_h = (int)xd->h; p.a_w = (int)xd->w;
   p.g_n = (int)yd->n; p.g_h = (int)yd->h; p.g_w = (int)yd->w;
   p.a_step = stride;
   p.nth = k; p.ntw = k;
   p.dh0 = -pad; p.dhs = 1; p.dw0 = -pad; p.dws = 1;
-  p.kh0 = 0; p.khs = 1; p.kw0 = 0; p.kws = 1; p.kw_size = k;
-  p.w = w; p.w_sn = xd->c * k * k; p.w_sc = (int64_t)k * k; p.n = (int)yd->c;
+  p.kh0 = 0; p.khs = 1; p.kw0 = 0; p.kws = 1; p.ksz = k;
+  p.w = wp; p.n = (int)yd->c;
+  p.a_bytes = act_bytes(xd);
+  p.w_bytes = (uint32_t)(vae2_conv2d_packed_size(yd->c, xd->c, k, 0) * 4);
   p.bias = bias;
-  p.y = y; p.y_ps = yd->ps; p.y_h = (int)yd->h; p.y_w = (int)yd->w;
+  p.y = y; p.y_ps = (int)yd->ps; p.y_h = (int)yd->h; p.y_w = (int)yd->w;
   p.y_step = 1; p.y_offh = 0; p.y_offw = 0;
   p.beta = beta;
   p.stats = stats;
   return launch_igemm(p, 0, as_stream(stream), fn);
 }
 
-int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* w,
+int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
                          float* dx, const vae2_act* dxd, int k, int stride,
                          int pad, float beta, void* stream) {
   const char* fn = "vae2_conv2d_bwd_data";
-  VAE2_REQUIRE(dy && w && dx, fn, "null pointer");
+  VAE2_REQUIRE(dy && wp && dx, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(dxd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
-  // One launch per (ph, pw) stride-parity class of the input pixels.
-  // Input row ih = stride*i + ph receives from output row oh = (ih + pad - kh)/stride
-  // for every kh with (ph + pad - kh) % stride == 0.
+  VAE2_REQUIRE(fits32(dxd) && fits32(dyd), fn, "tensor too large for 32-bit indexing");
+  // One launch per (ph, pw) stride-parity class of the input pixels: input row
+  // ih = stride*i + ph receives from output row oh = (ih + pad - kh)/stride for every
+  // kh with (ph + pad - kh) % stride == 0.
   for (int ph = 0; ph < stride; ++ph) {
     for (int pw = 0; pw < stride; ++pw) {
       int gh = (int)((dxd->h - ph + stride - 1) / stride);
       int gw = (int)((dxd->w - pw + stride - 1) / stride);
       if (gh <= 0 || gw <= 0) continue;
-      // valid kh: kh0, kh0+stride, ... < k, with (ph + pad - kh0) % stride == 0
       int kh0 = ((ph + pad) % stride + stride) % stride;
       int kw0 = ((pw + pad) % stride + stride) % stride;
       int nth = kh0 < k ? (k - 1 - kh0) / stride + 1 : 0;
       int ntw = kw0 < k ? (k - 1 - kw0) / stride + 1 : 0;
       IGemm p{};
-      p.a = dy; p.a_ps = dyd->ps; p.a_c = (int)dyd->c; p.a_h = (int)dyd->h; p.a_w = (int)dyd->w;
+      p.a = dy; p.a_ps = (int)dyd->ps; p.a_c = (int)dyd->c; p.a_c4 = round_up((int)dyd->c, 4);
+      p.a_h = (int)dyd->h; p.a_w = (int)dyd->w;
       p.g_n = (int)dxd->n; p.g_h = gh; p.g_w = gw;
       p.a_step = 1;
       p.nth = nth; p.ntw = ntw;
-      // oh = i + (ph + pad - kh)/stride ; kh = kh0 + th*stride -> d = d0 - th
       p.dh0 = (ph + pad - kh0) / stride; p.dhs = -1;
       p.dw0 = (pw + pad - kw0) / stride; p.dws = -1;
-      p.kh0 = kh0; p.khs = stride; p.kw0 = kw0; p.kws = stride; p.kw_size = k;
-      // B[n = ci][(t, c = co)] = w[co][ci][kh][kw]
-      p.w = w; p.w_sn = (int64_t)k * k; p.w_sc = dxd->c * k * k; p.n = (int)dxd->c;
+      p.kh0 = kh0; p.khs = stride; p.kw0 = kw0; p.kws = stride; p.ksz = k;
+      p.w = wp; p.n = (int)dxd->c;
+      p.a_bytes = act_bytes(dyd);
+      p.w_bytes = (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4);
       p.bias = nullptr;
-      p.y = dx; p.y_ps = dxd->ps; p.y_h = (int)dxd->h; p.y_w = (int)dxd->w;
+      p.y = dx; p.y_ps = (int)dxd->ps; p.y_h = (int)dxd->h; p.y_w = (int)dxd->w;
       p.y_step = stride; p.y_offh = ph; p.y_offw = pw;
       p.beta = beta;
       p.stats = nullptr;
@@ -590,15 +601,13 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* w,
   return 0;
 }
 
-int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd,
-                                       int k) {
+int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, int k) {
   if (!act_ok(xd) || !act_ok(dyd)) return 0;
-  int ncol = (int)(k * k * xd->c);
-  WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol);
-  int64_t part = t.splits * dyd->c * ncol;
+  int ncol4 = k * k * round_up((int)xd->c, 4);
+  WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol4);
+  int64_t part = (int64_t)t.splits * dyd->c * ncol4;
   int64_t bias_part = 2 * vae2_bn_partial_rows(dyd) * dyd->c;
-  int64_t bias_sums = 2 * dyd->c * 2;  // doubles as floats
-  return part + bias_part + bias_sums + 4;
+  return part + bias_part + 4;
 }
 
 int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
@@ -608,18 +617,24 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   const char* fn = "vae2_conv2d_bwd_weight";
   VAE2_REQUIRE(x && dy && dw && ws, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(xd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
+  VAE2_REQUIRE(fits32(xd) && fits32(dyd), fn, "tensor too large for 32-bit indexing");
   VAE2_REQUIRE(ws_size >= vae2_conv2d_bwd_weight_ws_size(xd, dyd, k), fn, "workspace too small");
   hipStream_t s = as_stream(stream);
-  int ncol = (int)(k * k * xd->c);
-  WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol);
+  const int cin4 = round_up((int)xd->c, 4);
+  const int ncol4 = k * k * cin4;
+  WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol4);
   WGrad p{};
-  p.x = x; p.x_ps = xd->ps; p.cin = (int)xd->c; p.x_h = (int)xd->h; p.x_w = (int)xd->w;
-  p.dy = dy; p.dy_ps = dyd->ps; p.cout = (int)dyd->c;
+  p.x = x; p.x_ps = (int)xd->ps; p.cin = (int)xd->c; p.cin4 = cin4;
+  p.x_h = (int)xd->h; p.x_w = (int)xd->w;
+  p.dy = dy; p.dy_ps = (int)dyd->ps; p.cout = (int)dyd->c;
   p.o_n = (int)dyd->n; p.o_h = (int)dyd->h; p.o_w = (int)dyd->w;
   p.k = k; p.stride = stride; p.pad = pad;
-  p.P = act_pixels(dyd);
+  p.P = (int)act_pixels(dyd);
   p.px_split = t.px_split;
   p.part = ws;
+  p.ohw_div = FastDiv((uint32_t)(dyd->h * dyd->w));
+  p.ow_div = FastDiv((uint32_t)dyd->w);
+  p.cin4_div = FastDiv((uint32_t)cin4);
   dim3 grid(t.gx, t.gy, (unsigned)t.splits);
   switch (t.tm) {
     case 1: launch_wgrad_tn<1>(p, t.tn, grid, s); break;
@@ -629,17 +644,18 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   }
   int rc = check_launch(fn);
   if (rc) return rc;
-  int64_t total = (int64_t)dyd->c * ncol;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ew_blocks(total)), dim3(256), 0, s,
-                     (const float*)ws, t.splits, (int)dyd->c, (int)xd->c, k, dw, accumulate);
+  int64_t total = dyd->c * xd->c * k * k;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0, s,
+                     (const float*)ws, t.splits, (int)dyd->c, (int)xd->c, cin4, k, dw,
+                     accumulate);
   rc = check_launch(fn);
   if (rc) return rc;
   if (dbias) {
-    float* bp = ws + t.splits * dyd->c * ncol;
+    float* bp = ws + (int64_t)t.splits * dyd->c * ncol4;
     rc = vae2_bn_stats(dy, dyd, bp, stream);
     if (rc) return rc;
-    rc = bias_grad_from_partials(bp, vae2_bn_partial_rows(dyd), dyd->c, dbias,
-                                      accumulate, stream);
+    rc = bias_grad_from_partials(bp, vae2_bn_partial_rows(dyd), dyd->c, dbias, accumulate,
+                                 stream);
     if (rc) return rc;
   }
   return 0;

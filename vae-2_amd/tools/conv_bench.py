@@ -1,0 +1,105 @@
+"""Per-shape timing of the conv kernels (forward, data-grad, weight-grad) with HIP events.
+
+    python tools/conv_bench.py [--batch 8] [--iters 20]
+
+Shapes are the dominant ones of the 128x256 ELBO step; the
+FLOP count is the algorithmic 2*M*N*K of each GEMM.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+import torch  # noqa: E402
+
+from vae2 import _lib, ops  # noqa: E402
+from vae2._lib import call  # noqa: E402
+
+SHAPES = [  # H, W, Cin, Cout, k, stride, count per step (App. B, fwd)
+    (128, 256, 64, 64, 3, 1, 12),
+    (128, 256, 270, 270, 1, 1, 9),
+    (128, 256, 64, 256, 1, 1, 12),
+    (128, 256, 18, 18, 3, 1, 96),
+    (64, 128, 36, 36, 3, 1, 96),
+    (32, 64, 72, 72, 3, 1, 80),
+    (16, 32, 144, 144, 3, 1, 32),
+    (128, 256, 256, 18, 3, 1, 4),
+    (128, 256, 256, 64, 1, 1, 4),
+    (128, 256, 18, 36, 3, 2, 24),
+]
+
+
+def timeit(fn, iters):
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    lib = _lib.load()
+    dev = "cuda"
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    print(f"{'shape':34s} {'fwd us':>8s} {'TF/s':>6s} {'dgrad us':>9s} {'TF/s':>6s} "
+          f"{'wgrad us':>9s} {'TF/s':>6s}")
+    for H, W, ci, co, k, st, cnt in SHAPES:
+        B = a.batch
+        x = ops.new_act((B, H, W, ci), torch.empty(1, device=dev))
+        x.normal_()
+        oh, ow = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
+        w = torch.randn(co, ci, k, k, device=dev) * 0.05
+        y = ops.new_act((B, oh, ow, co), x)
+        dy = ops.new_act((B, oh, ow, co), x)
+        dy.normal_()
+        dx = ops.new_act((B, H, W, ci), x)
+        dw = torch.zeros_like(w)
+        wp0 = ops.packed_weight(w, 0)
+        wp1 = ops.packed_weight(w, 1)
+        xp, xa = ops.act_of(x)
+        yp, ya = ops.act_of(y)
+        dyp, dya = ops.act_of(dy)
+        dxp, dxa = ops.act_of(dx)
+        pad = k // 2
+        size = lib.vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xa), ctypes.byref(dya), k)
+        ws = torch.empty(size, device=dev)
+        s = ops.stream_ptr()
+        flops = 2.0 * B * oh * ow * co * ci * k * k
+
+        def fwd():
+            call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ops.ptr(wp0), None, yp,
+                 ctypes.byref(ya), k, st, pad, 0.0, None, s)
+
+        def dgrad():
+            call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ops.ptr(wp1), dxp,
+                 ctypes.byref(dxa), k, st, pad, 0.0, s)
+
+        def wgrad():
+            call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya),
+                 ops.ptr(dw), None, k, st, pad, 0, ops.ptr(ws), size, s)
+
+        tf, td, tw = timeit(fwd, a.iters), timeit(dgrad, a.iters), timeit(wgrad, a.iters)
+        tot["fwd"] += tf * cnt
+        tot["dgrad"] += td * cnt
+        tot["wgrad"] += tw * cnt
+        name = f"{H}x{W} {ci}->{co} k{k}s{st} x{cnt}"
+        print(f"{name:34s} {tf:8.1f} {flops / tf / 1e6:6.1f} {td:9.1f} {flops / td / 1e6:6.1f} "
+              f"{tw:9.1f} {flops / tw / 1e6:6.1f}", flush=True)
+    print("weighted per-step ms (listed shapes only):",
+          {k_: round(v / 1e3, 2) for k_, v in tot.items()})
+
+
+if __name__ == "__main__":
+    main()

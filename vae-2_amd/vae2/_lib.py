@@ -31,6 +31,8 @@ P_ACT = ctypes.POINTER(Act)
 _SIGS = {
     "vae2_abi_version": (c_int, []),
     "vae2_last_error": (ctypes.c_char_p, []),
+    "vae2_conv2d_packed_size": (c_i64, [c_i64, c_i64, c_int, c_int]),
+    "vae2_conv2d_pack_weight": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp]),
     "vae2_conv2d_fwd_stats_rows": (c_i64, [P_ACT, c_i64]),
     "vae2_conv2d_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                 c_f32, c_vp, c_vp]),

@@ -77,6 +77,15 @@ def _empty(shape, like, dtype=_F32):
     return torch.empty(shape, dtype=dtype, device=like.device)
 
 
+def new_act(shape, like):
+    """Uninitialised NHWC activation (N,H,W,C) whose pixel stride is rounded up to
+    a multiple of 4 channels (16-byte aligned pixels: the conv kernels' vector path)."""
+    n, h, w, c = shape
+    cp = (c + 3) // 4 * 4
+    buf = torch.empty((n, h, w, cp), dtype=_F32, device=like.device)
+    return buf if cp == c else buf[..., :c]
+
+
 def _grad_sink(p):
     """(buffer to accumulate a parameter gradient into, value autograd should get)."""
     if p is None or not p.requires_grad:
@@ -131,18 +140,28 @@ class ConvSpec:
                 (w + 2 * self.pad - self.k) // self.stride + 1)
 
 
+def packed_weight(weight, mode):
+    """Weights in the kernels' packed layout (mode 0: forward, 1: data gradient)."""
+    cout, cin, k, _ = weight.shape
+    out = torch.empty((_lib.load().vae2_conv2d_packed_size(cout, cin, k, mode),),
+                      dtype=_F32, device=weight.device)
+    call("vae2_conv2d_pack_weight", ptr(weight), cout, cin, k, mode, ptr(out), stream_ptr())
+    return out
+
+
 def _conv_fwd(x, weight, bias, spec, stats=None):
     xp, xa = act_of(x)
     n, h, w, _ = x.shape
     oh, ow = spec.out_hw(h, w)
     cout = weight.shape[0]
-    y = _empty((n, oh, ow, cout), x)
+    y = new_act((n, oh, ow, cout), x)
     yp, ya = act_of(y)
     timer = prof.active()
     ev = None
     if timer is not None and timer.matches(n, oh, ow, cout):
         ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k)
-    call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(weight), ptr(bias), yp, ctypes.byref(ya),
+    wp = packed_weight(weight, 0)
+    call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(wp), ptr(bias), yp, ctypes.byref(ya),
          spec.k, spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
     if ev is not None:
         ev.record(torch.cuda.current_stream())
@@ -166,9 +185,10 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx):
              ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
     dx = None
     if need_dx:
-        dx = _empty(tuple(x.shape), x)
+        dx = new_act(tuple(x.shape), x)
         dxp, dxa = act_of(dx)
-        call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(weight), dxp, ctypes.byref(dxa),
+        wp = packed_weight(weight, 1)
+        call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp, ctypes.byref(dxa),
              spec.k, spec.stride, spec.pad, 0.0, s)
     return dx, wret, bret
 
@@ -203,7 +223,7 @@ class _ConvBN(torch.autograd.Function):
             save = _empty((4 * cout,), x)
             call("vae2_bn_eval_coeffs", ptr(gamma), ptr(beta), ptr(bn.running_mean),
                  ptr(bn.running_var), spec.eps, cout, ptr(save), s)
-        y = _empty((n, oh, ow, cout), x)
+        y = new_act((n, oh, ow, cout), x)
         rp, ra = act_of(r)
         yp, ya = act_of(y)
         if residual is not None:
@@ -245,11 +265,11 @@ class _ConvBN(torch.autograd.Function):
         if gsink is not None or bsink is not None:
             call("vae2_bn_bwd_param_grads", ptr(lsums), cout, ptr(gsink), ptr(bsink), s)
         gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
-        dr = _empty(tuple(r.shape), r)
+        dr = new_act(tuple(r.shape), r)
         drp, dra = act_of(dr)
         dres = None
         if ctx.has_res and ctx.needs_input_grad[5]:
-            dres = _empty(tuple(r.shape), r)
+            dres = new_act(tuple(r.shape), r)
             dresp, dresa = act_of(dres)
         else:
             dresp, dresa = None, dra
@@ -290,7 +310,7 @@ def conv(x, conv_mod):
 
 # ------------------------------------------------------------- fuse / cat ----
 def _up_bwd(g, shape):
-    dx = _empty(shape, g)
+    dx = new_act(shape, g)
     gp, ga = act_of(g)
     dxp, dxa = act_of(dx)
     call("vae2_upsample_bilinear_bwd", gp, ctypes.byref(ga), dxp, ctypes.byref(dxa), 0.0,
@@ -303,7 +323,7 @@ class _FuseSum(torch.autograd.Function):
     def forward(ctx, out_hw, *terms):
         ref = terms[0]
         n, c = ref.shape[0], ref.shape[3]
-        y = _empty((n, out_hw[0], out_hw[1], c), ref)
+        y = new_act((n, out_hw[0], out_hw[1], c), ref)
         ptrs = (ctypes.c_void_p * len(terms))()
         acts = (Act * len(terms))()
         for i, t in enumerate(terms):
@@ -320,7 +340,7 @@ class _FuseSum(torch.autograd.Function):
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
         dy = as_act(dy)
-        g = _empty(tuple(y.shape), y)
+        g = new_act(tuple(y.shape), y)
         dyp, dya = act_of(dy)
         yp, ya = act_of(y)
         gp, ga = act_of(g)
@@ -350,7 +370,7 @@ class _UpCat(torch.autograd.Function):
         x0 = xs[0]
         n, h, w, _ = x0.shape
         ctot = sum(t.shape[3] for t in xs)
-        y = _empty((n, h, w, ctot), x0)
+        y = new_act((n, h, w, ctot), x0)
         s = stream_ptr()
         off = 0
         for t in xs:
@@ -401,7 +421,7 @@ class _Cat(torch.autograd.Function):
         ref = parts[0]
         n = ref.shape[0]
         ctot = sum(p_.shape[3] for p_ in parts)
-        y = _empty((n, out_hw[0], out_hw[1], ctot), ref)
+        y = new_act((n, out_hw[0], out_hw[1], ctot), ref)
         s = stream_ptr()
         off = 0
         for p_, tile in zip(parts, tiles):
@@ -466,7 +486,7 @@ class _AvgPool(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         dy = as_act(dy)
-        dx = _empty(ctx.shape, dy)
+        dx = new_act(ctx.shape, dy)
         dyp, dya = act_of(dy)
         dxp, dxa = act_of(dx)
         call("vae2_global_avgpool_bwd", dyp, ctypes.byref(dya), dxp, ctypes.byref(dxa), 0.0,
@@ -484,7 +504,7 @@ class _ToNHWC(torch.autograd.Function):
     def forward(ctx, x):
         x = x.contiguous()
         n, c, h, w = x.shape
-        y = _empty((n, h, w, c), x)
+        y = new_act((n, h, w, c), x)
         yp, ya = act_of(y)
         call("vae2_nchw_to_nhwc", ptr(x), yp, ctypes.byref(ya), 0.0, stream_ptr())
         return y
@@ -512,7 +532,7 @@ class _ToNCHW(torch.autograd.Function):
     def backward(ctx, dy):
         dy = dy.contiguous()
         n, c, h, w = dy.shape
-        dx = _empty((n, h, w, c), dy)
+        dx = new_act((n, h, w, c), dy)
         dxp, dxa = act_of(dx)
         call("vae2_nchw_to_nhwc", ptr(dy), dxp, ctypes.byref(dxa), 0.0, stream_ptr())
         return dx
@@ -567,7 +587,7 @@ class _L1(torch.autograd.Function):
         else:
             pp, pa = act_of(p)
             tp, ta = act_of(t)
-            dp = _empty(tuple(p.shape), p)
+            dp = new_act(tuple(p.shape), p)
             dpp, da = act_of(dp)
         call("vae2_l1_bwd", pp, ctypes.byref(pa), tp, ctypes.byref(ta), ptr(gout), ctx.scale, dpp,
              ctypes.byref(da), 0.0, stream_ptr())
@@ -584,7 +604,7 @@ class _ReparamKL(torch.autograd.Function):
     def forward(ctx, muvar, eps, prior, scale):
         n, h, w, c2 = muvar.shape
         zc = c2 // 2
-        z = _empty((n, h, w, zc), muvar)
+        z = new_act((n, h, w, zc), muvar)
         kl = _empty((), muvar)
         mp, ma = act_of(muvar)
         ep, ea = act_of(eps)
@@ -600,7 +620,7 @@ class _ReparamKL(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, dkl):
         muvar, eps = ctx.saved_tensors
-        dm = _empty(tuple(muvar.shape), muvar)
+        dm = new_act(tuple(muvar.shape), muvar)
         mp, ma = act_of(muvar)
         ep, ea = act_of(eps)
         dmp, dma = act_of(dm)
