@@ -323,8 +323,11 @@ static int64_t igemm_rows(int64_t M, int N) {
 }
 
 // ------------------------------------------------------------ wgrad ----
-// One wave per workgroup.  Tile: 16*TM output channels x 16*TN (tap, cin4) columns,
-// over a pixel range; partial tile -> part[split][cout][ncol4] (ncol4 = k*k*cin4).
+// dW[co][(tap, ci4)] = sum_p dY[p][co] * X[src(p, tap)][ci].  MFMA m = co, n = column,
+// k = pixel: lane group g takes pixels 4g..4g+3 of each 16-pixel chunk.
+// Workgroup = 4 waves sharing one (co, column) tile; wave w takes chunks w, w+4, ...
+// of the workgroup's pixel range, the 4 partial tiles are summed in LDS (fixed
+// order) and written as one fp32 slab part[split][cout][ncol4].
 struct WGrad {
   const float* x;
   int x_ps, cin, cin4, x_h, x_w;
@@ -332,37 +335,41 @@ struct WGrad {
   int dy_ps, cout, o_n, o_h, o_w;
   int k, stride, pad;
   int P, px_split;
+  uint32_t x_bytes, dy_bytes;
   float* part;
   FastDiv ohw_div, ow_div, cin4_div;
 };
 
 template <int TM, int TN>
-__global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
+  extern __shared__ __attribute__((aligned(16))) float wred[];  // [3][TM*TN*4][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int ncol4 = p.k * p.k * p.cin4;
   const int co0 = blockIdx.y * 16 * TM;
   const int col0 = blockIdx.x * 16 * TN;
   const int pbeg = blockIdx.z * p.px_split;
   const int pend = min(pbeg + p.px_split, p.P);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
 
   int aco[TM];
-  bool aok[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    aco[i] = co0 + i * 16 + r;
-    aok[i] = aco[i] < p.cout;
+    const int co = co0 + i * 16 + r;
+    aco[i] = co < p.cout ? co : -1;
   }
-  int bkh[TN], bkw[TN], bci[TN];
+  int bkh[TN], bkw[TN], boff[TN];
   bool bok[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    int col = col0 + j * 16 + r;
-    int t = (int)p.cin4_div.div((uint32_t)col);
-    bci[j] = col - t * p.cin4;
+    const int col = col0 + j * 16 + r;
+    const int t = (int)p.cin4_div.div((uint32_t)col);
+    const int ci = col - t * p.cin4;
     bkh[j] = t / p.k;
     bkw[j] = t - bkh[j] * p.k;
-    bok[j] = col < ncol4 && bci[j] < p.cin;
+    bok[j] = col < ncol4 && ci < p.cin;
+    boff[j] = (bkh[j] * p.x_w + bkw[j]) * p.x_ps + ci;
   }
   f4 acc[TM][TN];
 #pragma unroll
@@ -371,7 +378,7 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int ohw = p.o_h * p.o_w;
-  for (int pc = pbeg; pc < pend; pc += 16) {
+  for (int pc = pbeg + 16 * wave; pc < pend; pc += 64) {
     f4 fa[TM], fb[TN];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -382,16 +389,18 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
       const int rem = pp - n * ohw;
       const int oh = (int)p.ow_div.div((uint32_t)rem);
       const int ow = rem - oh * p.o_w;
-      const float* dyrow = p.dy + pp * p.dy_ps;
+      const uint32_t drow = (uint32_t)(pp * p.dy_ps);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i][s] = (pv && aok[i]) ? dyrow[aco[i]] : 0.f;
+      for (int i = 0; i < TM; ++i)
+        fa[i][s] = load1(dr, (pv && aco[i] >= 0) ? (drow + aco[i]) * 4u : kOOB);
       const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
-      const int xbase = n * p.x_h;
+      const int xc = ((n * p.x_h + ih0) * p.x_w + iw0) * p.x_ps;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int ih = ih0 + bkh[j], iw = iw0 + bkw[j];
-        const bool ok = pv && bok[j] && ih >= 0 && ih < p.x_h && iw >= 0 && iw < p.x_w;
-        fb[j][s] = ok ? p.x[((xbase + ih) * p.x_w + iw) * p.x_ps + bci[j]] : 0.f;
+        const bool ok = pv && bok[j] && (unsigned)ih < (unsigned)p.x_h &&
+                        (unsigned)iw < (unsigned)p.x_w;
+        fb[j][s] = load1(xr, ok ? (uint32_t)(xc + boff[j]) * 4u : kOOB);
       }
     }
 #pragma unroll
@@ -402,6 +411,29 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   }
+
+  // cross-wave reduction in a fixed order: waves 1..3 park their tiles in LDS
+  constexpr int NV = TM * TN * 4;
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          wred[((wave - 1) * NV + (i * TN + j) * 4 + e) * 64 + lane] = acc[i][j][e];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[i][j][e] += wred[(w * NV + (i * TN + j) * 4 + e) * 64 + lane];
 
   float* out = p.part + (int64_t)blockIdx.z * p.cout * ncol4;
 #pragma unroll
@@ -419,24 +451,37 @@ __global__ __launch_bounds__(64) void wgrad_kernel(WGrad p) {
 }
 
 // dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin4 + ci]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int cout,
-                                    int cin, int cin4, int k, float* __restrict__ dw,
-                                    int accumulate) {
+// Block = 4 waves x 64 slab columns: lane = column (coalesced 256-B rows per split),
+// wave w sums splits w, w+4, ...; the 4 partial sums are combined in LDS in order.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                           int splits, int cout, int cin,
+                                                           int cin4, int k,
+                                                           float* __restrict__ dw,
+                                                           int accumulate) {
+  __shared__ float red[4][64];
   const int kk = k * k;
   const int ncol4 = kk * cin4;
-  const int total = cout * cin * kk;  // over the OIHW gradient
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
-    const int co = idx / (cin * kk);
-    const int rem = idx - co * cin * kk;
-    const int ci = rem / kk;
-    const int t = rem - ci * kk;
-    const int64_t src = (int64_t)co * ncol4 + t * cin4 + ci;
-    const int64_t stride = (int64_t)cout * ncol4;
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += part[sp * stride + src];
-    dw[idx] = accumulate ? dw[idx] + s : s;
+  const int total = cout * ncol4;  // slab elements
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (idx < total) {
+    const float* src = part + idx;
+    const int64_t stride = (int64_t)total;
+#pragma unroll 8
+    for (int sp = wave; sp < splits; sp += 4) s += src[sp * stride];
   }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || idx >= total) return;
+  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  const int co = idx / ncol4;
+  const int col = idx - co * ncol4;
+  const int t = col / cin4;
+  const int ci = col - t * cin4;
+  if (ci >= cin) return;
+  const int64_t o = ((int64_t)co * cin + ci) * kk + t;
+  dw[o] = accumulate ? dw[o] + s : s;
 }
 
 struct WTile {
@@ -449,26 +494,28 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   t.tm = mt <= 4 ? mt : 4;
   t.gy = (int)ceil_div(cout, 16 * t.tm);
   int ct = (ncol4 + 15) / 16;
-  t.tn = ct <= 4 ? ct : 4;
+  const int tn_max = t.tm == 4 ? 3 : 4;  // <4,4> would not fit 2 waves/SIMD without spills
+  t.tn = ct <= tn_max ? ct : tn_max;
   t.gx = (int)ceil_div(ncol4, 16 * t.tn);
   int64_t tiles = (int64_t)t.gx * t.gy;
-  // ~4096 waves in flight, at least 512 pixels (32 chunks) per wave
-  int64_t want = ceil_div(4096, tiles);
-  int64_t maxs = ceil_div(P, 512);
+  // ~1024 workgroups (4 waves each), at least 1024 pixels (16 chunks per wave) each
+  int64_t want = ceil_div(1024, tiles);
+  int64_t maxs = ceil_div(P, 1024);
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;
-  t.px_split = (int)(ceil_div(ceil_div(P, s), 16) * 16);
+  t.px_split = (int)(ceil_div(ceil_div(P, s), 64) * 64);
   t.splits = (int)ceil_div(P, t.px_split);
   return t;
 }
 
 template <int TM>
 static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
+  const size_t lds = (size_t)3 * TM * 4 * 4 * 64 * sizeof(float) / 4 * tn;  // 3 waves x NV x 64
   switch (tn) {
-    case 1: hipLaunchKernelGGL((wgrad_kernel<TM, 1>), grid, dim3(64), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((wgrad_kernel<TM, 2>), grid, dim3(64), 0, s, p); break;
-    case 3: hipLaunchKernelGGL((wgrad_kernel<TM, 3>), grid, dim3(64), 0, s, p); break;
-    default: hipLaunchKernelGGL((wgrad_kernel<TM, 4>), grid, dim3(64), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p); break;
+    case 2: hipLaunchKernelGGL((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p); break;
+    case 3: hipLaunchKernelGGL((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p); break;
+    default: hipLaunchKernelGGL((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p); break;
   }
 }
 
@@ -632,6 +679,8 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   p.P = (int)act_pixels(dyd);
   p.px_split = t.px_split;
   p.part = ws;
+  p.x_bytes = act_bytes(xd);
+  p.dy_bytes = act_bytes(dyd);
   p.ohw_div = FastDiv((uint32_t)(dyd->h * dyd->w));
   p.ow_div = FastDiv((uint32_t)dyd->w);
   p.cin4_div = FastDiv((uint32_t)cin4);
@@ -644,8 +693,8 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   }
   int rc = check_launch(fn);
   if (rc) return rc;
-  int64_t total = dyd->c * xd->c * k * k;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0, s,
+  int64_t slab = dyd->c * (int64_t)ncol4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 64)), dim3(256), 0, s,
                      (const float*)ws, t.splits, (int)dyd->c, (int)xd->c, cin4, k, dw,
                      accumulate);
   rc = check_launch(fn);
