@@ -16,7 +16,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import ops, streams
 from ._lib import call
 
 _SYNC_BN_GROUP = None
@@ -66,6 +66,7 @@ def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
     """Mean-reduce the flat gradient buffers over all ranks."""
     if not is_dist():
         return
+    streams.join_all()
     ws = world_size()
     for f in flats:
         g = f.grad

@@ -17,13 +17,14 @@ on NHWC activations:
   decoders   trunk + z code map + heads (:849-963)             -> x3t_hat, xt_hat
   z-net      trunk + upsample/cat/avgpool/1x1 head (:1070-1122) -> mu|logvar
 """
+import contextlib
 import logging
 import os
 
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, streams
 
 BN_MOMENTUM = 0.01
 logger = logging.getLogger(__name__)
@@ -432,9 +433,13 @@ class HighResolutionNetED(HighResolutionNet):
                 out["decp_" + k] = v
         return out
 
-    def encode(self, x, z, code):
+    def encode_trunk(self, x):
+        """Encoder stem .. stage 3 + transition3 (independent of z)."""
+        return self._trunk_to_stage4_inputs("", x)
+
+    def encode(self, x, z, code, trunk=None):
         """x: (N,H,W,3L) NHWC -> x2t_hat (N,H,W,3*NUM_CLASSES)."""
-        xs = self._trunk_to_stage4_inputs("", x)
+        xs = trunk if trunk is not None else self._trunk_to_stage4_inputs("", x)
         if self.enable_random_code:
             codes = [code, z] if not self.is_baseline else [z]
             xs = self._apply_codes("", xs, codes)
@@ -448,15 +453,15 @@ class HighResolutionNetED(HighResolutionNet):
         ys = run_stage(getattr(self, prefix + "stage4"), xs)
         return self._heads(prefix, ys)
 
-    def run(self, x, z=None, code=None, is_baseline=False):
-        x2t = self.encode(x, z, code)
-        if is_baseline:
-            with torch.no_grad():
-                x3t = self.decode("decf_", x2t, z)
+    def run(self, x, z=None, code=None, is_baseline=False, trunk=None):
+        """Encoder then both decoders; the past decoder runs on a side stream
+        concurrently with the future decoder (they are independent)."""
+        x2t = self.encode(x, z, code, trunk)
+        with torch.no_grad() if is_baseline else contextlib.nullcontext():
+            with streams.on_side(1, inputs=[x2t, z]) as sp:
                 x1t = self.decode("decp_", x2t, z)
-        else:
             x3t = self.decode("decf_", x2t, z)
-            x1t = self.decode("decp_", x2t, z)
+            streams.join(sp, [x1t])
         return x1t, x2t, x3t
 
     def forward(self, x, z=None, is_baseline=False, code=None):

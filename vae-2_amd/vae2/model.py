@@ -21,7 +21,7 @@ read to `check_anomalies()` (one sync instead of four per step).
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, streams
 
 _MODES = ("VAE_NATIVE", "VAE_ANNEAL", "VAE_GAN", "DETERMINISTIC")
 
@@ -74,6 +74,7 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
 
     def check_anomalies(self):
         """Host-read the deferred NaN/Inf flag (raises AssertionError like the reference)."""
+        streams.join_all()
         if self._flag is not None:
             bad = int(self._flag.item())
             self._flag.zero_()
@@ -108,26 +109,33 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
         x3t_n = ops.to_nhwc(x3t)
         H, W = xt_n.shape[1:3]
 
+        enc_in = ops.cat([xt_n, x2t_n], (H, W)) if is_baseline else xt_n
         z = None
         kl = None
+        trunk = None
         if baseline_mode != "DETERMINISTIC":
             zin = [xt_n, x2t_n, x3t_n] if is_baseline else [xt_n, x3t_n]
-            muvars = self.encz_model.run(ops.cat(zin, (H, W)))
-            hd = isinstance(muvars, list)
-            eps_shapes = ([(B, zc, m.shape[1], m.shape[2]) for m in muvars] if hd
-                          else (B, zc, 1, 1))
-            code_shape = (B, zc, 1, 1) if ed.enable_random_code else None
-            eps, code = self._draw(eps_shapes, code_shape, dev, prior)
-            mvs = muvars if hd else [muvars]
-            epss = eps if hd else [eps]
-            zs, kls = [], []
-            for mv, e in zip(mvs, epss):
-                e_n = e.to(dev, non_blocking=True).permute(0, 2, 3, 1).contiguous()
-                zb, klb = ops.reparam_kl(mv, e_n, prior=prior, scale=1.0 / B)
-                zs.append(zb)
-                kls.append(klb)
-            z = zs if hd else zs[0]
-            kl = kls[0] if len(kls) == 1 else ops.weighted_sum(kls, [1.0] * len(kls))
+            # posterior net + sampler on a side stream, concurrent with the encoder
+            # trunk (stem .. stage 3 do not depend on z)
+            with streams.on_side(0, inputs=zin) as sz:
+                muvars = self.encz_model.run(ops.cat(zin, (H, W)))
+                hd = isinstance(muvars, list)
+                eps_shapes = ([(B, zc, m.shape[1], m.shape[2]) for m in muvars] if hd
+                              else (B, zc, 1, 1))
+                code_shape = (B, zc, 1, 1) if ed.enable_random_code else None
+                eps, code = self._draw(eps_shapes, code_shape, dev, prior)
+                mvs = muvars if hd else [muvars]
+                epss = eps if hd else [eps]
+                zs, kls = [], []
+                for mv, e in zip(mvs, epss):
+                    e_n = e.to(dev, non_blocking=True).permute(0, 2, 3, 1).contiguous()
+                    zb, klb = ops.reparam_kl(mv, e_n, prior=prior, scale=1.0 / B)
+                    zs.append(zb)
+                    kls.append(klb)
+                z = zs if hd else zs[0]
+                kl = kls[0] if len(kls) == 1 else ops.weighted_sum(kls, [1.0] * len(kls))
+            trunk = ed.encode_trunk(enc_in)
+            streams.join(sz, [zs, kl, muvars])
             if not prior:
                 self._check([("0", z)] if not hd else list(zip(map(str, range(len(zs))), zs)))
         else:
@@ -137,8 +145,7 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
         code_n = (code.to(dev, non_blocking=True).permute(0, 2, 3, 1).contiguous()
                   if code is not None else None)
 
-        enc_in = ops.cat([xt_n, x2t_n], (H, W)) if is_baseline else xt_n
-        x1p, x2p, x3p = ed.run(enc_in, z, code_n, is_baseline)
+        x1p, x2p, x3p = ed.run(enc_in, z, code_n, is_baseline, trunk)
         self._check([("xt_predict", x1p), ("x2t_predict", x2p), ("x3t_predict", x3p)])
 
         terms, lams = [], []

@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from . import ops
+from . import ops, streams
 from ._lib import call
 from .params import flatten
 
@@ -33,6 +33,7 @@ class FusedAdam:
                               "differentiable": False, "fused": None}]
 
     def zero_grad(self, set_to_none=False):
+        streams.join_all()
         for f in self.flats:
             f.zero_grad()
 
@@ -40,6 +41,7 @@ class FusedAdam:
     def step(self):
         self.lr = float(self.param_groups[0]["lr"])
         self.step_count += 1
+        streams.join_all()
         s = ops.stream_ptr()
         for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
             call("vae2_adam_step", ops.ptr(f.data), ops.ptr(f.grad), ops.ptr(m), ops.ptr(v),
