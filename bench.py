@@ -13,11 +13,14 @@ L1 x3 + KL, backward, RCCL gradient all-reduce (N > 1, SyncBN statistics),
 Adam.  frames/s = clips * 9 / step time, whole job.
 
 Printed JSON also carries:
-  roofline      the dominant kernel (the igemm conv instantiation that runs the
+  roofline      the dominant conv kernel (the igemm instantiation that runs the
                 64->64 3x3 full-resolution convs), timed live with HIP events
-                around its launches in the timed region; achieved = algorithmic
-                FLOPs per launch / average launch time, against the fp32 matrix
-                peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+                around its launches during --roofline-steps extra steps that follow
+                the timed region (each timed launch isolated from the side streams,
+                so the span is the kernel's own execution, as rocprof measures it);
+                achieved = algorithmic FLOPs per launch / average launch time,
+                against the fp32 matrix peak (157.3 TFLOP/s, MI355X_MICROARCH.md);
+                traffic = HBM bytes per launch from the committed PMC measurement.
   cpu_baseline  the CPU oracle (oracle/ref_cpu.py, the reference's ops on CPU)
                 timed on this host's cores, rank 0 at N=1 only, on a bounded sample.
 """
@@ -52,7 +55,25 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-steps", type=int, default=3)
     return ap.parse_args()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC measurement
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark), else None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == kernel.replace("void ", ""):
+            best = d
+    return best
 
 
 def cpu_baseline(args):
@@ -133,19 +154,13 @@ def main():
     torch.cuda.synchronize()
     fm.check_anomalies()
 
-    kname = prof.fwd_kernel_name(B, H, W, 64)
-    timer = prof.KernelTimer(kname)
+    # ---- timed region: the metric (full stream concurrency, no instrumentation) ----
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if args.no_roofline:
-        for _ in range(args.steps):
-            loss = step()
-    else:
-        with timer:
-            for _ in range(args.steps):
-                loss = step()
+    for _ in range(args.steps):
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -156,6 +171,18 @@ def main():
         elapsed = float(t)
     fm.check_anomalies()
     last_loss = float(loss)
+
+    # ---- roofline phase: the same step, the dominant kernel's launches timed with
+    # HIP events on their stream, each launch isolated from the side streams ----
+    kname = prof.fwd_kernel_name(B, H, W, 64)
+    timer = prof.KernelTimer(kname)
+    if not args.no_roofline and args.roofline_steps > 0:
+        torch.cuda.synchronize()
+        with timer:
+            for _ in range(args.roofline_steps):
+                step()
+        torch.cuda.synchronize()
+        fm.check_anomalies()
 
     if rank == 0:
         ms = 1e3 * elapsed / args.steps
@@ -177,13 +204,19 @@ def main():
         }
         summ = timer.summary() if not args.no_roofline else None
         if summ:
+            tr = pmc_traffic(kname)
             out["roofline"] = {"bound": "mfma", "kernel": kname,
                                "achieved": round(summ["tflops"], 3), "peak": FP32_MFMA_PEAK_TF,
                                "unit": "TFLOP/s",
                                "frac": round(summ["tflops"] / FP32_MFMA_PEAK_TF, 4),
-                               "traffic": None, "avg_launch_us": round(summ["avg_us"], 2),
+                               "traffic": round(tr["hbm_bytes_per_launch"]) if tr else None,
+                               "traffic_unit": "bytes/launch (PMC)",
+                               "avg_launch_us": round(summ["avg_us"], 2),
                                "flops_per_launch": summ["flops_per_launch"],
-                               "launches": summ["launches"]}
+                               "algorithmic_bytes_per_launch": summ["bytes_per_launch"],
+                               "launches": summ["launches"],
+                               "measured": f"{args.roofline_steps} steps after the timed region, "
+                                           "launches isolated from side streams"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -27,11 +27,53 @@ import torch
 import torch.nn.functional as F
 
 
+SYNC_GROUP = None  # set to a torch.distributed group for SyncBatchNorm semantics
+
+
 def _bn(x, bn):
     if bn.training and bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
+    if SYNC_GROUP is not None and bn.training:
+        return _sync_bn(x, bn)
     return F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
                         bn.training or not bn.track_running_stats, bn.momentum, bn.eps)
+
+
+class _SyncStats(torch.autograd.Function):
+    """all_reduce(sum) of per-rank statistics with an all_reduce(sum) backward
+    (nn.SyncBatchNorm's gradient exchange, train.py:216-218)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        import torch.distributed as dist
+        out = t.clone()
+        dist.all_reduce(out, group=SYNC_GROUP)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        import torch.distributed as dist
+        g = g.clone()
+        dist.all_reduce(g, group=SYNC_GROUP)
+        return g
+
+
+def _sync_bn(x, bn):
+    """Training BatchNorm with statistics over all ranks (nn.SyncBatchNorm)."""
+    n_local = torch.tensor([float(x.numel() // x.shape[1])], dtype=x.dtype)
+    s = torch.cat([x.sum(dim=(0, 2, 3)), (x * x).sum(dim=(0, 2, 3)), n_local])
+    s = _SyncStats.apply(s)
+    c = x.shape[1]
+    cnt = s[2 * c].detach()
+    mean = s[:c] / cnt
+    var = s[c:2 * c] / cnt - mean * mean
+    with torch.no_grad():
+        m = bn.momentum
+        bn.running_mean.mul_(1 - m).add_(m * mean.detach())
+        bn.running_var.mul_(1 - m).add_(m * var.detach() * cnt / (cnt - 1))
+    shape = (1, c, 1, 1)
+    xh = (x - mean.view(shape)) / torch.sqrt(var.view(shape) + bn.eps)
+    return xh * bn.weight.view(shape) + bn.bias.view(shape)
 
 
 def _conv(x, c):

@@ -1,0 +1,108 @@
+"""Data-parallel path on CPU: world size 2 over gloo (multi-GPU runs are the
+driver's).  Covers the SyncBN statistics exchange, the bucketed gradient
+all-reduce, and the invariant the reference's SyncBN + DDP setup guarantees
+(SURVEY.md §4): N ranks x B/N clips == 1 rank x B clips, checked against the
+reference's own golden vectors."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+
+
+def _w_stats(rank, world, port, q):
+    _init(rank, world, port)
+    from vae2 import ops
+    local = torch.arange(6, dtype=torch.float64) * (rank + 1)
+    out, count = ops._all_reduce_sums(local, 10.0, dist.group.WORLD)
+    q.put((rank, out.tolist(), count))
+    dist.destroy_process_group()
+
+
+def _w_bucket(rank, world, port, q):
+    _init(rank, world, port)
+    from vae2 import dist as vdist
+    buf = torch.full((1000,), float(rank + 1))
+    vdist.bucket_allreduce(buf, bucket_elems=128)
+    q.put((rank, float(buf.min()), float(buf.max())))
+    dist.destroy_process_group()
+
+
+def _w_invariant(rank, world, port, q):
+    _init(rank, world, port)
+    from helpers import build, golden, make_cfg, t
+    from oracle import ref_cpu
+    g = golden("tiny_native")
+    ed, ez = build(make_cfg("tiny"))
+    sl = slice(rank, rank + 1)  # one clip per rank
+    ref_cpu.SYNC_GROUP = dist.group.WORLD
+    terms, preds, _ = ref_cpu.elbo(ez, ed, t(g["xt"])[sl], t(g["x2t"])[sl], t(g["x3t"])[sl],
+                                   t(g["eps"])[sl], t(g["code"])[sl])
+    loss = terms["loss_all"].detach().clone()
+    dist.all_reduce(loss)
+    q.put((rank, float(loss) / world, [p.detach()[0].numpy() for p in preds]))
+    dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_sync_bn_sums_gloo():
+    res = _run(_w_stats)
+    for _, out, count in res:
+        assert out == [3.0 * i for i in range(6)]
+        assert count == 20.0
+
+
+def test_bucketed_grad_allreduce_gloo():
+    for _, lo, hi in _run(_w_bucket):
+        assert lo == hi == 3.0
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_equal_one_rank_with_sync_bn():
+    """2 ranks x 1 clip with SyncBN == the reference's 1 rank x 2 clips (golden)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import golden
+    g = golden("tiny_native")
+    res = _run(_w_invariant)
+    for _, loss, _ in res:
+        assert abs(loss - float(g["loss_loss_all"])) <= 1e-5 * abs(float(g["loss_loss_all"]))
+    for rank, _, preds in res:
+        np.testing.assert_allclose(preds[1], g["x2p"][rank], rtol=0, atol=1e-4 * np.abs(g["x2p"]).max())

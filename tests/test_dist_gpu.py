@@ -1,0 +1,77 @@
+"""The HIP data-parallel path with SyncBN: 2 ranks sharing one MI355X (gloo
+process group on device tensors; RCCL refuses two ranks per GPU, the driver's
+8-GPU runs use RCCL).  Invariant: 2 ranks x 1 clip == the
+reference's 1 rank x 2 clips; after the gradient all-reduce both ranks hold the
+same gradients."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from helpers import build, golden, make_cfg, t
+    from vae2 import dist as vdist
+    from vae2.model import FullModel_encdec
+    from vae2.optim import FusedAdam
+    dev = "cuda:0"
+    vdist.set_sync_bn(True)
+    g = golden("tiny_native")
+    ed, ez = build(make_cfg("tiny"))
+    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(dev)
+    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-4)
+    sl = slice(rank, rank + 1)
+    fm.set_noise(t(g["eps"])[sl], t(g["code"])[sl])
+    opt.zero_grad()
+    losses, x1p, x2p, x3p = fm(t(g["xt"])[sl].to(dev), t(g["x2t"])[sl].to(dev),
+                               t(g["x3t"])[sl].to(dev), 1.0)
+    losses[0].backward()
+    vdist.allreduce_grads(opt.flats)
+    torch.cuda.synchronize()
+    loss = losses[0].detach().clone()
+    dist.all_reduce(loss)
+    gsum = torch.cat([f.grad for f in opt.flats]).double().sum().item()
+    q.put((rank, float(loss) / world, x2p[0].cpu().numpy(), x3p[0].cpu().numpy(), gsum))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu_sync_bn_matches_reference():
+    from helpers import golden
+    g = golden("tiny_native")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = float(g["loss_loss_all"])
+    for rank, loss, x2p, x3p, _ in res:
+        assert abs(loss - ref) <= 1e-5 * abs(ref)
+        np.testing.assert_allclose(x2p, g["x2p"][rank], rtol=0, atol=1e-4 * np.abs(g["x2p"]).max())
+        assert np.linalg.norm(x3p - g["x3p"][rank]) <= 1e-3 * np.linalg.norm(g["x3p"][rank])
+    assert res[0][4] == res[1][4]  # identical averaged gradients on both ranks

@@ -42,6 +42,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// Bijective blockIdx remap (T1): blocks are dealt round-robin over the 8 XCDs, so
+// logical tiles are re-numbered to make each XCD own a contiguous run of tiles
+// (vertically adjacent image rows share that XCD's L2).  Speed only.
+__device__ __forceinline__ int xcd_remap(int orig, int n) {
+  const int q = n >> 3, rr = n & 7, x = orig & 7;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (orig >> 3);
+}
+
 __device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
@@ -101,7 +109,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int M = p.g_n * p.g_h * p.g_w;
-  const int mw = (blockIdx.x * 4 + wave) * (16 * TM);
+  const int bm = xcd_remap(blockIdx.x, gridDim.x);
+  const int mw = (bm * 4 + wave) * (16 * TM);
   const int n0 = blockIdx.y * BN;
   const int kk4 = p.ksz * p.ksz * p.a_c4;
 
@@ -252,8 +261,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
       if (n0 + c >= p.n) continue;
       float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
       float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-      p.stats[blockIdx.x * p.n + n0 + c] = s;
-      p.stats[(rows + blockIdx.x) * p.n + n0 + c] = s2;
+      p.stats[bm * p.n + n0 + c] = s;
+      p.stats[(rows + bm) * p.n + n0 + c] = s2;
     }
   }
 }

@@ -44,9 +44,20 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--md", default=None)
+    ap.add_argument("--kernel", default=None,
+                    help="also report this kernel's average over its last --last dispatches")
+    ap.add_argument("--last", type=int, default=0)
     a = ap.parse_args()
     if a.path.endswith(".db"):
         rows = from_db(a.path)
+    elif os.path.isdir(a.path):
+        import glob
+        f = glob.glob(os.path.join(a.path, "**", "*kernel_trace.csv"), recursive=True)[0]
+        rows = []
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((short(r["Kernel_Name"]), int(r["Start_Timestamp"]),
+                             int(r["End_Timestamp"])))
     else:
         rows = []
         with open(a.path) as f:
@@ -54,6 +65,14 @@ def main():
                 rows.append((short(r["Kernel_Name"]), int(r["Start_Timestamp"]),
                              int(r["End_Timestamp"])))
     out, total, span = summarise(rows)
+    extra = []
+    if a.kernel:
+        ds = sorted((s_, e_) for n, s_, e_ in rows if n.replace("void ", "") == a.kernel)
+        sel = ds[-a.last:] if a.last else ds
+        if sel:
+            avg = sum(e_ - s_ for s_, e_ in sel) / len(sel)
+            extra = ["", f"`{a.kernel}`: {len(ds)} dispatches in total, average over the last "
+                         f"{len(sel)} (the bench's roofline phase): {avg / 1e3:.1f} us"]
     lines = [f"kernels: {len(rows)} dispatches, {total / 1e6:.2f} ms total kernel time, "
              f"span {span / 1e6:.2f} ms",
              "",
@@ -62,6 +81,7 @@ def main():
     for n, c, tt, av, mn, mx in out[:a.top]:
         lines.append(f"| `{n}` | {c} | {tt / 1e6:.3f} | {av / 1e3:.1f} | {mn / 1e3:.1f} | "
                      f"{mx / 1e3:.1f} | {100 * tt / total:.1f} |")
+    lines += extra
     text = "\n".join(lines)
     print(text)
     if a.md:

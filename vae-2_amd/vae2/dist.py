@@ -62,18 +62,24 @@ def sync_bn_group():
 BUCKET_ELEMS = 8 * 1024 * 1024  # 32 MB fp32 buckets
 
 
+def bucket_allreduce(buf, bucket_elems=BUCKET_ELEMS, group=None):
+    """Sum-all-reduce a flat buffer in fixed-size buckets (same bucket boundaries on
+    every rank, issued in order)."""
+    n = buf.numel()
+    for off in range(0, n, bucket_elems):
+        dist.all_reduce(buf[off:off + bucket_elems], group=group)
+
+
 def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
-    """Mean-reduce the flat gradient buffers over all ranks."""
+    """Mean-reduce the flat gradient buffers over all ranks (DDP semantics)."""
     if not is_dist():
         return
     streams.join_all()
     ws = world_size()
     for f in flats:
         g = f.grad
-        n = g.numel()
-        for off in range(0, n, bucket_elems):
-            dist.all_reduce(g[off:off + bucket_elems])
-        call("vae2_scale", ops.ptr(g), ops.ptr(g), n, 1.0 / ws, ops.stream_ptr())
+        bucket_allreduce(g, bucket_elems)
+        call("vae2_scale", ops.ptr(g), ops.ptr(g), g.numel(), 1.0 / ws, ops.stream_ptr())
 
 
 def reduce_tensor(inp):

@@ -159,12 +159,15 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     timer = prof.active()
     ev = None
     if timer is not None and timer.matches(n, oh, ow, cout):
-        ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k)
+        # algorithmic: 2*M*N*K flops; bytes = input read once + output written once + weights
+        ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k,
+                          4.0 * (n * h * w * xa.c + n * oh * ow * cout +
+                                 cout * xa.c * spec.k * spec.k))
     wp = packed_weight(weight, 0)
     call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(wp), ptr(bias), yp, ctypes.byref(ya),
          spec.k, spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
     if ev is not None:
-        ev.record(torch.cuda.current_stream())
+        timer.finish(ev)
     return y
 
 

@@ -30,6 +30,7 @@ class KernelTimer:
         self.kernel_name = kernel_name
         self.events = []
         self.flops = []
+        self.bytes = []
         self.enabled = False
         self._names = {}
 
@@ -50,13 +51,27 @@ class KernelTimer:
             self._names[key] = fwd_kernel_name(n, oh, ow, cout)
         return self._names[key] == self.kernel_name
 
-    def record(self, flops):
+    def record(self, flops, nbytes=0.0):
+        """Start timing one launch on the current stream.  The launch is isolated
+        from the side streams (they are waited for before it, and wait for it
+        after) so the event span is the kernel's own execution, as rocprof sees it,
+        not time spent queued behind a concurrent stream."""
+        from . import streams
+        streams.join_all()
+        self.bytes.append(nbytes)
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record(torch.cuda.current_stream())
         self.events.append((s, e))
         self.flops.append(flops)
         return e
+
+    @staticmethod
+    def finish(ev):
+        from . import streams
+        cur = torch.cuda.current_stream()
+        ev.record(cur)
+        streams.fence_side(cur)
 
     def summary(self):
         torch.cuda.synchronize()
@@ -67,4 +82,5 @@ class KernelTimer:
         tot_ms = sum(ms)
         return {"launches": n, "avg_us": 1e3 * tot_ms / n,
                 "flops_per_launch": sum(self.flops) / n,
+                "bytes_per_launch": sum(self.bytes) / n,
                 "tflops": sum(self.flops) / (tot_ms * 1e-3) / 1e12}

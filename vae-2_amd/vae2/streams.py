@@ -56,12 +56,25 @@ def join(stream, outputs=()):
     _record(outputs, main)
 
 
+def fence_side(stream):
+    """Make every other stream of the device wait for `stream`'s current work."""
+    for (dev, _), s in _SIDE.items():
+        if dev == str(stream.device) and s != stream:
+            s.wait_stream(stream)
+    main = torch.cuda.default_stream(stream.device)
+    if main != stream:
+        main.wait_stream(stream)
+
+
 def join_all():
     """Make the current stream wait for every side stream (e.g. before the optimizer
     step: parameter gradients are written by backward kernels on side streams)."""
-    if not _SIDE or not torch.cuda.is_available():
+    if not torch.cuda.is_available():
         return
     main = torch.cuda.current_stream()
     for (dev, _), s in _SIDE.items():
-        if dev == str(main.device):
+        if dev == str(main.device) and s != main:
             main.wait_stream(s)
+    d = torch.cuda.default_stream(main.device)
+    if d != main:
+        main.wait_stream(d)
