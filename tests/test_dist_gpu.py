@@ -25,6 +25,15 @@ def _port():
 
 
 def _worker(rank, world, port, q):
+    try:
+        _work(rank, world, port, q)
+    except BaseException as e:  # report instead of leaving the parent waiting
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+
+
+def _work(rank, world, port, q):
     import sys
     for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -50,12 +59,13 @@ def _worker(rank, world, port, q):
     vdist.allreduce_grads(opt.flats)
     torch.cuda.synchronize()
     loss = losses[0].detach().clone()
-    dist.all_reduce(loss)
+    vdist.all_reduce_(loss)
     gsum = torch.cat([f.grad for f in opt.flats]).double().sum().item()
-    q.put((rank, float(loss) / world, x2p[0].cpu().numpy(), x3p[0].cpu().numpy(), gsum))
+    q.put((rank, float(loss) / world, x2p[0].detach().cpu().numpy(), x3p[0].detach().cpu().numpy(), gsum))
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(300)
 def test_two_ranks_one_gpu_sync_bn_matches_reference():
     from helpers import golden
     g = golden("tiny_native")
@@ -65,10 +75,24 @@ def test_two_ranks_one_gpu_sync_bn_matches_reference():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=600) for _ in procs], key=lambda r: r[0])
+    import queue
+    import time
+    res, deadline = [], time.time() + 240
+    while len(res) < len(procs):
+        try:
+            res.append(q.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"2-rank run failed: exit codes {[p.exitcode for p in procs]}, "
+                            f"results so far {res}")
     for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+        p.join(timeout=60)
+    errors = [r for r in res if r[1] == "error"]
+    assert not errors, errors[0][2]
+    res = sorted(res, key=lambda r: r[0])
     ref = float(g["loss_loss_all"])
     for rank, loss, x2p, x3p, _ in res:
         assert abs(loss - ref) <= 1e-5 * abs(ref)

@@ -62,12 +62,23 @@ def sync_bn_group():
 BUCKET_ELEMS = 8 * 1024 * 1024  # 32 MB fp32 buckets
 
 
+def all_reduce_(t, group=None):
+    """In-place sum all-reduce.  RCCL ("nccl") reduces device buffers directly; a gloo
+    group (CPU CI, several ranks sharing one GPU) is fed through host staging."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
 def bucket_allreduce(buf, bucket_elems=BUCKET_ELEMS, group=None):
     """Sum-all-reduce a flat buffer in fixed-size buckets (same bucket boundaries on
     every rank, issued in order)."""
     n = buf.numel()
     for off in range(0, n, bucket_elems):
-        dist.all_reduce(buf[off:off + bucket_elems], group=group)
+        all_reduce_(buf[off:off + bucket_elems], group=group)
 
 
 def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):

@@ -105,8 +105,9 @@ def _bn_group():
 def _all_reduce_sums(sums, count, group):
     if group is None:
         return sums, count
+    from . import dist as vdist
     out = sums.clone()
-    dist.all_reduce(out, group=group)
+    vdist.all_reduce_(out, group=group)
     return out, count * dist.get_world_size(group)
 
 
