@@ -10,7 +10,10 @@ frames, 8 clips per GPU (weak scaling; 64 clips at 8 GPUs), fp32, random-init
 weights (seed 0, the reference's init), synthetic Gaussian clips resident in HBM.
 One step = posterior net + reparameterisation + encoder + 2 decoders forward,
 L1 x3 + KL, backward, RCCL gradient all-reduce (N > 1, SyncBN statistics),
-Adam.  frames/s = clips * 9 / step time, whole job.
+Adam.  frames/s = clips * 9 / step time, whole job.  At N=1 the step is
+captured once as a HIP graph (vae2.graph.StepGraph: same kernels, one launch,
+bit-identical to eager steps — tests/test_graph_gpu.py) and replayed; the noise
+is drawn on the device inside the step so every replay samples fresh noise.
 
 Printed JSON also carries:
   roofline      the dominant conv kernel (the igemm instantiation that runs the
@@ -56,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay the step as one captured HIP graph (auto: at N=1)")
     return ap.parse_args()
 
 
@@ -140,15 +145,21 @@ def main():
     xs = [torch.randn(B, 3 * L, H, W, generator=g).to(dev) for _ in range(3)]
     zc = ez.z_dim
 
-    def step():
+    def eager_step():
         opt.zero_grad()
-        fm.set_noise(torch.randn(B, zc, 1, 1), torch.randn(B, zc, 1, 1))
+        fm.set_noise(torch.randn(B, zc, 1, 1, device=dev), torch.randn(B, zc, 1, 1, device=dev))
         losses = fm(*xs, 1.0)[0]
         losses[0].backward()
         vdist.allreduce_grads(opt.flats)
         opt.step()
         return losses[0]
 
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    step = eager_step
+    if use_graph:
+        from vae2.graph import StepGraph
+        graph = StepGraph(eager_step, warmup=2)
+        step = graph.replay
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -180,7 +191,7 @@ def main():
         torch.cuda.synchronize()
         with timer:
             for _ in range(args.roofline_steps):
-                step()
+                eager_step()
         torch.cuda.synchronize()
         fm.check_anomalies()
 
@@ -199,7 +210,8 @@ def main():
                                    f"{B} clips/GPU x {3 * L} frames (CLIP_LENGTH={L})",
                        "global_batch": world * B, "frames_per_clip": 3 * L,
                        "image": [H, W], "parallelism": f"dp{world}",
-                       "sync_bn": world > 1},
+                       "sync_bn": world > 1,
+                       "launch": "hip_graph" if use_graph else "eager"},
             "last_loss": last_loss,
         }
         summ = timer.summary() if not args.no_roofline else None
@@ -216,7 +228,7 @@ def main():
                                "algorithmic_bytes_per_launch": summ["bytes_per_launch"],
                                "launches": summ["launches"],
                                "measured": f"{args.roofline_steps} steps after the timed region, "
-                                           "launches isolated from side streams"}
+                                           "launches isolated from side streams (eager)"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

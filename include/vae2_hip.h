@@ -52,6 +52,16 @@ int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode);
 int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k,
                             int mode, float* out, void* stream);
 
+/* Many packings in one launch (a model's whole weight set after each optimizer
+ * step).  `jobs` is a DEVICE array of njobs descriptors; `out` buffers must not
+ * overlap.  Replaces the per-conv weight reads of F.conv2d (enc_hrnet.py:27-30). */
+typedef struct vae2_pack_job {
+  const float* w;  /* [cout][cin][k][k] */
+  float* out;      /* vae2_conv2d_packed_size(cout, cin, k, mode) floats */
+  int32_t cout, cin, k, mode;
+} vae2_pack_job;
+int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* stream);
+
 /* y = conv2d(x, w, stride, pad) (+ bias) (+ beta*y) with w packed (mode 0),
  * optional per-channel BN partial sums of the result in `stats` ([2][rows][cout]).
  * Replaces nn.Conv2d.forward: conv3x3 enc_hrnet.py:27-30, Bottleneck 1x1
@@ -109,6 +119,20 @@ int vae2_bn_finalize(const double* sums, double count, const float* gamma,
                      const float* beta, float* running_mean, float* running_var,
                      int64_t* num_batches_tracked, float momentum, float eps,
                      int64_t c, float* save, void* stream);
+
+/* vae2_bn_partials_reduce + vae2_bn_finalize in one launch (no cross-rank
+ * exchange in between: single GPU, or BN without SyncBN).                      */
+int vae2_bn_reduce_finalize(const float* partials, int64_t rows, int64_t c,
+                            double* sums, double count, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int64_t* num_batches_tracked, float momentum, float eps,
+                            float* save, void* stream);
+
+/* Backward: partials [2][rows][c] of (sum g, sum g*xhat) -> sums [2][c] (double)
+ * and dgamma += sum g*xhat, dbeta += sum g, in one launch.                       */
+int vae2_bn_bwd_reduce_param_grads(const float* partials, int64_t rows, int64_t c,
+                                   double* sums, float* dgamma, float* dbeta,
+                                   void* stream);
 
 /* Eval mode: save [4][c] from running statistics.                              */
 int vae2_bn_eval_coeffs(const float* gamma, const float* beta,
@@ -234,6 +258,16 @@ int vae2_nonfinite_check(const float* x, int64_t n, int32_t* flag,
 int vae2_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
                    float lr, float beta1, float beta2, float eps,
                    float weight_decay, int64_t step, void* stream);
+
+/* The same step with the step counter and learning rate in device memory, so a
+ * captured HIP graph can replay it: vae2_adam_coeffs increments state[0] (step,
+ * double) and writes coeffs = {lr/(1-b1^step), sqrt(1-b2^step)} from lr = state[1];
+ * vae2_adam_step_dev then updates each flat buffer from those coefficients.    */
+int vae2_adam_coeffs(double* state, float beta1, float beta2, float* coeffs,
+                     void* stream);
+int vae2_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n,
+                       const float* coeffs, float beta1, float beta2, float eps,
+                       float weight_decay, void* stream);
 
 /* dst = src * scale, for fp32 buffers (grad averaging after all-reduce).       */
 int vae2_scale(float* dst, const float* src, int64_t n, float scale,

@@ -123,6 +123,58 @@ __global__ __launch_bounds__(256) void partials_reduce_kernel(
   }
 }
 
+// One block per channel: reduce partial rows (double, fixed order), then either
+// finalize (MODE 0: mean/invstd/scale/shift + running stats) or write the sums and
+// accumulate dgamma/dbeta (MODE 1: backward).  Used when no cross-rank exchange
+// sits between the reduction and its consumer.
+template <int MODE>
+__global__ __launch_bounds__(256) void reduce_then_kernel(
+    const float* __restrict__ part, int64_t rows, int64_t C, double* sums, double count,
+    const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
+    float momentum, float eps, float* save, float* dgamma, float* dbeta) {
+  __shared__ double red[2][4];
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int64_t r = tid; r < rows; r += 256) {
+    a += (double)part[r * C + c];
+    b += (double)part[(rows + r) * C + c];
+  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = a;
+    red[1][tid >> 6] = b;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  const double s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const double s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  sums[c] = s0;
+  sums[C + c] = s1;
+  if (MODE == 1) {
+    if (dgamma) dgamma[c] += (float)s1;
+    if (dbeta) dbeta[c] += (float)s0;
+    return;
+  }
+  if (c == 0 && nbt) nbt[0] += 1;
+  const double mean = s0 / count;
+  double var = s1 / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)eps);
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float bt = beta ? beta[c] : 0.f;
+  save[c] = (float)mean;
+  save[C + c] = (float)invstd;
+  save[2 * C + c] = (float)(gm * invstd);
+  save[3 * C + c] = (float)(bt - mean * (gm * invstd));
+  if (rmean) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unbiased);
+  }
+}
+
 __global__ void bn_finalize_kernel(const double* sums, double count,
                                    const float* gamma, const float* beta,
                                    float* rmean, float* rvar, int64_t* nbt,
@@ -315,6 +367,32 @@ int vae2_bn_finalize(const double* sums, double count, const float* gamma,
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
                      as_stream(stream), sums, count, gamma, beta, running_mean,
                      running_var, num_batches_tracked, momentum, eps, c, save);
+  return check_launch(fn);
+}
+
+int vae2_bn_reduce_finalize(const float* partials, int64_t rows, int64_t c,
+                            double* sums, double count, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int64_t* num_batches_tracked, float momentum, float eps,
+                            float* save, void* stream) {
+  const char* fn = "vae2_bn_reduce_finalize";
+  VAE2_REQUIRE(partials && sums && save && rows > 0 && c > 0 && count > 0, fn, "bad arguments");
+  VAE2_REQUIRE((running_mean == nullptr) == (running_var == nullptr), fn,
+               "running_mean and running_var must both be set or both be null");
+  hipLaunchKernelGGL((reduce_then_kernel<0>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
+                     partials, rows, c, sums, count, gamma, beta, running_mean, running_var,
+                     num_batches_tracked, momentum, eps, save, (float*)nullptr, (float*)nullptr);
+  return check_launch(fn);
+}
+
+int vae2_bn_bwd_reduce_param_grads(const float* partials, int64_t rows, int64_t c,
+                                   double* sums, float* dgamma, float* dbeta, void* stream) {
+  const char* fn = "vae2_bn_bwd_reduce_param_grads";
+  VAE2_REQUIRE(partials && sums && rows > 0 && c > 0, fn, "bad arguments");
+  hipLaunchKernelGGL((reduce_then_kernel<1>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
+                     partials, rows, c, sums, 1.0, (const float*)nullptr, (const float*)nullptr,
+                     (float*)nullptr, (float*)nullptr, (int64_t*)nullptr, 0.f, 0.f, (float*)nullptr,
+                     dgamma, dbeta);
   return check_launch(fn);
 }
 

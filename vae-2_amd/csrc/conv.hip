@@ -82,6 +82,29 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int ci
   }
 }
 
+// One block row (blockIdx.y) per packing job.
+__global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pack_job* jobs) {
+  const vae2_pack_job j = jobs[blockIdx.y];
+  const int kk = j.k * j.k;
+  const int rows = j.mode == 0 ? (j.cout + 63) / 64 * 64 : (j.cin + 63) / 64 * 64;
+  const int cols4 = j.mode == 0 ? (j.cin + 3) / 4 * 4 : (j.cout + 3) / 4 * 4;
+  const int per_row = kk * cols4;
+  const int total = rows * per_row;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int n = i / per_row;
+    const int rem = i - n * per_row;
+    const int t = rem / cols4;
+    const int c = rem - t * cols4;
+    float v = 0.f;
+    if (j.mode == 0) {
+      if (n < j.cout && c < j.cin) v = j.w[((int64_t)n * j.cin + c) * kk + t];
+    } else {
+      if (n < j.cin && c < j.cout) v = j.w[((int64_t)c * j.cin + n) * kk + t];
+    }
+    j.out[i] = v;
+  }
+}
+
 // ------------------------------------------------------------ igemm ----
 struct IGemm {
   const float* a;  // gathered activation (NHWC)
@@ -572,6 +595,14 @@ int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k, in
   int64_t total = vae2_conv2d_packed_size(cout, cin, k, mode);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0,
                      as_stream(stream), w, (int)cout, (int)cin, k * k, mode, out);
+  return check_launch(fn);
+}
+
+int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* stream) {
+  const char* fn = "vae2_conv2d_pack_weights";
+  VAE2_REQUIRE(jobs && njobs > 0 && njobs <= 65535, fn, "bad job table");
+  hipLaunchKernelGGL(pack_weights_batched_kernel, dim3(32, (unsigned)njobs), dim3(256), 0,
+                     as_stream(stream), jobs);
   return check_launch(fn);
 }
 

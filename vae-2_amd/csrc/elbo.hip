@@ -173,6 +173,41 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   }
 }
 
+// Device-resident step counter for graph replay: state = {step, lr} (double),
+// coeffs = {lr / (1 - b1^step), sqrt(1 - b2^step)} (float), as vae2_adam_step's host math.
+__global__ void adam_coeffs_kernel(double* state, float b1, float b2, float* coeffs) {
+  const double step = state[0] + 1.0;
+  state[0] = step;
+  const double lr = (double)(float)state[1];
+  coeffs[0] = (float)(lr / (1.0 - pow((double)b1, step)));
+  coeffs[1] = (float)sqrt(1.0 - pow((double)b2, step));
+}
+
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ m,
+                                                       float* __restrict__ v, int64_t n,
+                                                       const float* __restrict__ coeffs,
+                                                       float b1, float b2, float eps, float wd) {
+  const float lr_corr = coeffs[0];
+  const float bc2_sqrt = coeffs[1];
+  const float w1 = 1.f - b1;
+  const float w2 = 1.f - b2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    float pi = p[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);
+    float vi = v[i] * b2 + w2 * (gi * gi);
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi + (-lr_corr) * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
 __global__ void scale_kernel(float* dst, const float* src, int64_t n, float s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -293,6 +328,26 @@ int vae2_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
   hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
                      as_stream(stream), p, g, m, v, n, lr_corr, beta1, beta2, eps,
                      weight_decay, bc2s);
+  return check_launch(fn);
+}
+
+int vae2_adam_coeffs(double* state, float beta1, float beta2, float* coeffs,
+                     void* stream) {
+  const char* fn = "vae2_adam_coeffs";
+  VAE2_REQUIRE(state && coeffs, fn, "null pointer");
+  hipLaunchKernelGGL(adam_coeffs_kernel, dim3(1), dim3(1), 0, as_stream(stream), state, beta1,
+                     beta2, coeffs);
+  return check_launch(fn);
+}
+
+int vae2_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n,
+                       const float* coeffs, float beta1, float beta2, float eps,
+                       float weight_decay, void* stream) {
+  const char* fn = "vae2_adam_step_dev";
+  VAE2_REQUIRE(p && g && m && v && coeffs && n >= 0, fn, "bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
+                     as_stream(stream), p, g, m, v, n, coeffs, beta1, beta2, eps, weight_decay);
   return check_launch(fn);
 }
 

@@ -33,6 +33,7 @@ _SIGS = {
     "vae2_last_error": (ctypes.c_char_p, []),
     "vae2_conv2d_packed_size": (c_i64, [c_i64, c_i64, c_int, c_int]),
     "vae2_conv2d_pack_weight": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp]),
+    "vae2_conv2d_pack_weights": (c_int, [c_vp, c_i64, c_vp]),
     "vae2_conv2d_fwd_stats_rows": (c_i64, [P_ACT, c_i64]),
     "vae2_conv2d_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                 c_f32, c_vp, c_vp]),
@@ -47,6 +48,9 @@ _SIGS = {
     "vae2_bn_partials_reduce": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_vp]),
     "vae2_bn_finalize": (c_int, [c_vp, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32,
                                  c_i64, c_vp, c_vp]),
+    "vae2_bn_reduce_finalize": (c_int, [c_vp, c_i64, c_i64, c_vp, c_f64, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp, c_f32, c_f32, c_vp, c_vp]),
+    "vae2_bn_bwd_reduce_param_grads": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "vae2_bn_eval_coeffs": (c_int, [c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_vp, c_vp]),
     "vae2_bn_apply": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_vp, P_ACT, c_int, c_vp]),
     "vae2_bn_relu_bwd_reduce": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, c_int,
@@ -76,6 +80,9 @@ _SIGS = {
     "vae2_weighted_sum": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_f32), c_vp,
                                   c_vp]),
     "vae2_nonfinite_check": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "vae2_adam_coeffs": (c_int, [c_vp, c_f32, c_f32, c_vp, c_vp]),
+    "vae2_adam_step_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_f32, c_f32,
+                                   c_f32, c_vp]),
     "vae2_adam_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                                c_i64, c_vp]),
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
@@ -108,6 +115,12 @@ def load():
 
 def exported_symbols():
     return sorted(_SIGS)
+
+
+class PackJob(ctypes.Structure):
+    """vae2_pack_job (include/vae2_hip.h)."""
+    _fields_ = [("w", c_vp), ("out", c_vp), ("cout", ctypes.c_int32), ("cin", ctypes.c_int32),
+                ("k", ctypes.c_int32), ("mode", ctypes.c_int32)]
 
 
 class HipError(RuntimeError):

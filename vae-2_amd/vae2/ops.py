@@ -141,8 +141,69 @@ class ConvSpec:
                 (w + 2 * self.pad - self.k) // self.stride + 1)
 
 
+class PackPlan:
+    """Every Conv2d weight of a module tree in both packed layouts, refreshed by one
+    vae2_conv2d_pack_weights launch (FusedAdam calls run() after each update).
+
+    A weight's packed copy is used only while the weight is unchanged since the
+    last run (same storage, same autograd version counter); otherwise the conv
+    packs it itself, so in-place edits outside the optimizer stay correct."""
+
+    def __init__(self, module):
+        lib = _lib.load()
+        seen, self.weights = set(), []
+        for m in module.modules():
+            if isinstance(m, torch.nn.Conv2d) and id(m.weight) not in seen:
+                seen.add(id(m.weight))
+                self.weights.append(m.weight)
+        layout, total = [], 0
+        for w in self.weights:
+            cout, cin, k, _ = w.shape
+            sizes = [lib.vae2_conv2d_packed_size(cout, cin, k, mode) for mode in (0, 1)]
+            layout.append((total, sizes[0], total + sizes[0], sizes[1]))
+            total += sizes[0] + sizes[1]
+        self.buf = torch.empty((total,), dtype=_F32,
+                               device=self.weights[0].device if self.weights else None)
+        self._views = [(self.buf[a:a + na], self.buf[b:b + nb]) for a, na, b, nb in layout]
+        self._build_jobs()
+        self.run()
+
+    def _build_jobs(self):
+        if not self.weights:
+            self.njobs = 0
+            return
+        self._ptrs = [w.data_ptr() for w in self.weights]
+        jobs = (_lib.PackJob * (2 * len(self.weights)))()
+        for i, (w, views) in enumerate(zip(self.weights, self._views)):
+            cout, cin, k, _ = w.shape
+            for mode in (0, 1):
+                jobs[2 * i + mode] = _lib.PackJob(w.data_ptr(), views[mode].data_ptr(),
+                                                  cout, cin, k, mode)
+        host = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8)
+        self.jobs = host.to(self.buf.device)
+        self.njobs = len(jobs)
+
+    @torch.no_grad()
+    def run(self):
+        if not self.weights:
+            return
+        if any(w.data_ptr() != p for w, p in zip(self.weights, self._ptrs)):
+            self._build_jobs()
+        call("vae2_conv2d_pack_weights", ptr(self.jobs), self.njobs, stream_ptr())
+        for w, views in zip(self.weights, self._views):
+            w._vae2_packed = (views[0], views[1], w._version, w.data_ptr())
+
+    def bump_versions(self):
+        """Mark the weights modified (an in-place kernel wrote them) and re-pack."""
+        torch.autograd.graph.increment_version(self.weights)
+        self.run()
+
+
 def packed_weight(weight, mode):
     """Weights in the kernels' packed layout (mode 0: forward, 1: data gradient)."""
+    cached = getattr(weight, "_vae2_packed", None)
+    if cached is not None and cached[2] == weight._version and cached[3] == weight.data_ptr():
+        return cached[mode]
     cout, cin, k, _ = weight.shape
     out = torch.empty((_lib.load().vae2_conv2d_packed_size(cout, cin, k, mode),),
                       dtype=_F32, device=weight.device)
@@ -213,15 +274,25 @@ class _ConvBN(torch.autograd.Function):
             stats = _empty((2 * rows * cout,), x)
             r = _conv_fwd(x, weight, bias, spec, stats)
             sums = _empty((2 * cout,), x, torch.float64)
-            call("vae2_bn_partials_reduce", ptr(stats), rows, cout, ptr(sums), 0, s)
             group = _bn_group()
-            sums, count = _all_reduce_sums(sums, count, group)
             save = _empty((4 * cout,), x)
             track = bn.track_running_stats and bn.running_mean is not None
-            call("vae2_bn_finalize", ptr(sums), count, ptr(gamma), ptr(beta),
-                 ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
-                 ptr(bn.num_batches_tracked) if track else None, spec.momentum, spec.eps, cout,
-                 ptr(save), s)
+            stat_ptrs = (ptr(bn.running_mean) if track else None,
+                         ptr(bn.running_var) if track else None,
+                         ptr(bn.num_batches_tracked) if track else None)
+            if group is None:
+                if count <= 1:
+                    raise ValueError("Expected more than 1 value per channel when training, "
+                                     f"got input size {(n, cout, oh, ow)}")
+                call("vae2_bn_reduce_finalize", ptr(stats), rows, cout, ptr(sums), count,
+                     ptr(gamma), ptr(beta), *stat_ptrs, spec.momentum, spec.eps, ptr(save), s)
+            else:  # SyncBN: exchange the double sums between the reduction and finalize
+                call("vae2_bn_partials_reduce", ptr(stats), rows, cout, ptr(sums), 0, s)
+                sums, count = _all_reduce_sums(sums, count, group)
+                if count <= 1:
+                    raise ValueError("Expected more than 1 value per channel when training")
+                call("vae2_bn_finalize", ptr(sums), count, ptr(gamma), ptr(beta), *stat_ptrs,
+                     spec.momentum, spec.eps, cout, ptr(save), s)
         else:
             r = _conv_fwd(x, weight, bias, spec)
             save = _empty((4 * cout,), x)
@@ -263,11 +334,10 @@ class _ConvBN(torch.autograd.Function):
         call("vae2_bn_relu_bwd_reduce", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
              ctypes.byref(ra), ptr(save), int(spec.relu), ptr(part), s)
         lsums = _empty((2 * cout,), r, torch.float64)
-        call("vae2_bn_partials_reduce", ptr(part), rows, cout, ptr(lsums), 0, s)
         gsink, gret = _grad_sink(gamma)
         bsink, bret = _grad_sink(beta)
-        if gsink is not None or bsink is not None:
-            call("vae2_bn_bwd_param_grads", ptr(lsums), cout, ptr(gsink), ptr(bsink), s)
+        call("vae2_bn_bwd_reduce_param_grads", ptr(part), rows, cout, ptr(lsums), ptr(gsink),
+             ptr(bsink), s)
         gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
         dr = new_act(tuple(r.shape), r)
         drp, dra = act_of(dr)

@@ -1,8 +1,11 @@
 """Adam over flat parameter buffers (torch.optim.Adam semantics, train.py:251-261).
 
-One vae2_adam_step launch per flat buffer; the math follows torch.optim.Adam
+One vae2_adam_step_dev launch per flat buffer; the math follows torch.optim.Adam
 (lerp first moment, L2 weight decay folded into the gradient, bias corrections
-on the host).  state_dict() / load_state_dict() use torch.optim.Adam's format
+in double).  The step counter and learning rate live in device memory
+(vae2_adam_coeffs advances them), so the whole step can be captured in a HIP
+graph and replayed (vae2.graph.StepGraph); change the learning rate through
+param_groups[0]["lr"] and the next eager step() — or set_lr() between replays.  state_dict() / load_state_dict() use torch.optim.Adam's format
 (per-parameter exp_avg / exp_avg_sq / step) so optimizer checkpoints interchange.
 """
 import ctypes
@@ -19,11 +22,16 @@ class FusedAdam:
         if not isinstance(modules, (list, tuple)):
             modules = [modules]
         self.flats = [flatten(m) for m in modules]
+        # packed conv weights, refreshed in one launch per model after every update
+        self.packs = [ops.PackPlan(m) for m in modules]
         self.lr = float(lr)
         self.betas = (float(betas[0]), float(betas[1]))
         self.eps = float(eps)
         self.weight_decay = float(weight_decay)
-        self.step_count = 0
+        dev = self.flats[0].data.device
+        self._state = torch.zeros(2, dtype=torch.float64, device=dev)  # {step, lr}
+        self._coeffs = torch.zeros(2, dtype=torch.float32, device=dev)
+        self._dev_lr = None
         self.exp_avg = [torch.zeros_like(f.data) for f in self.flats]
         self.exp_avg_sq = [torch.zeros_like(f.data) for f in self.flats]
         self.param_groups = [{"params": [p for f in self.flats for p in f.params], "lr": self.lr,
@@ -37,25 +45,48 @@ class FusedAdam:
         for f in self.flats:
             f.zero_grad()
 
+    @property
+    def step_count(self):
+        return int(self._state[0].item())
+
+    @step_count.setter
+    def step_count(self, n):
+        self._state[0].fill_(float(n))
+
+    def set_lr(self, lr):
+        self.param_groups[0]["lr"] = float(lr)
+        self._sync_lr()
+
+    def _sync_lr(self):
+        lr = float(self.param_groups[0]["lr"])
+        self.lr = lr
+        if lr != self._dev_lr:  # eager: graphs read the device copy on replay
+            self._state[1].fill_(lr)
+            self._dev_lr = lr
+
     @torch.no_grad()
     def step(self):
-        self.lr = float(self.param_groups[0]["lr"])
-        self.step_count += 1
+        self._sync_lr()
         streams.join_all()
         s = ops.stream_ptr()
+        call("vae2_adam_coeffs", ops.ptr(self._state), self.betas[0], self.betas[1],
+             ops.ptr(self._coeffs), s)
         for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
-            call("vae2_adam_step", ops.ptr(f.data), ops.ptr(f.grad), ops.ptr(m), ops.ptr(v),
-                 f.numel, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
-                 self.step_count, s)
+            call("vae2_adam_step_dev", ops.ptr(f.data), ops.ptr(f.grad), ops.ptr(m), ops.ptr(v),
+                 f.numel, ops.ptr(self._coeffs), self.betas[0], self.betas[1], self.eps,
+                 self.weight_decay, s)
+        for plan in self.packs:
+            plan.bump_versions()
 
     # ---- torch.optim.Adam-compatible checkpoint format ----
     def state_dict(self):
         state = {}
         idx = 0
+        step = float(self.step_count)
         for f, m, v in zip(self.flats, self.exp_avg, self.exp_avg_sq):
             for p, off in zip(f.params, f.offsets):
                 n = p.numel()
-                state[idx] = {"step": torch.tensor(float(self.step_count)),
+                state[idx] = {"step": torch.tensor(step),
                               "exp_avg": m[off:off + n].view_as(p).clone(),
                               "exp_avg_sq": v[off:off + n].view_as(p).clone()}
                 idx += 1
@@ -80,7 +111,7 @@ class FusedAdam:
             self.step_count = max(steps)
         g = sd["param_groups"][0]
         self.param_groups[0]["lr"] = g.get("lr", self.lr)
-        self.lr = float(self.param_groups[0]["lr"])
+        self._sync_lr()
         self.betas = tuple(g.get("betas", self.betas))
         self.eps = g.get("eps", self.eps)
         self.weight_decay = g.get("weight_decay", self.weight_decay)

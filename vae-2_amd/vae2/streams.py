@@ -6,13 +6,16 @@ decoders.  Their low-resolution layers launch far fewer workgroups than the 256
 CUs, so running them on separate streams fills the GPU.  PyTorch autograd replays
 every backward op on the stream its forward op ran on, so the backward overlaps
 the same way.  Tensors crossing streams are registered with record_stream so the
-caching allocator never recycles them early.
+caching allocator never recycles them early.  Inside a HIP graph capture the
+side streams fork from and join back into the capture stream (event waits), so
+the captured graph keeps the same concurrency.
 """
 import contextlib
 
 import torch
 
 _SIDE = {}
+_FORKED = set()  # side streams forked into the capture in progress
 ENABLED = True
 
 
@@ -36,12 +39,14 @@ def _record(tensors, stream):
 @contextlib.contextmanager
 def on_side(idx, inputs=()):
     """Run the block on side stream `idx` after the current stream's prior work."""
-    if not ENABLED or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+    if not ENABLED or not torch.cuda.is_available():
         yield None
         return
     main = torch.cuda.current_stream()
     s = side_stream(main.device, idx)
     s.wait_stream(main)
+    if torch.cuda.is_current_stream_capturing():
+        _FORKED.add(s)
     _record(inputs, s)
     with torch.cuda.stream(s):
         yield s
@@ -61,6 +66,8 @@ def fence_side(stream):
     for (dev, _), s in _SIDE.items():
         if dev == str(stream.device) and s != stream:
             s.wait_stream(stream)
+    if torch.cuda.is_current_stream_capturing():
+        return  # the default stream is outside the graph; the capture stream joins at the end
     main = torch.cuda.default_stream(stream.device)
     if main != stream:
         main.wait_stream(stream)
@@ -72,9 +79,12 @@ def join_all():
     if not torch.cuda.is_available():
         return
     main = torch.cuda.current_stream()
+    capturing = torch.cuda.is_current_stream_capturing()
     for (dev, _), s in _SIDE.items():
-        if dev == str(main.device) and s != main:
+        if dev == str(main.device) and s != main and (not capturing or s in _FORKED):
             main.wait_stream(s)
+    if capturing:
+        return
     d = torch.cuda.default_stream(main.device)
     if d != main:
         main.wait_stream(d)
