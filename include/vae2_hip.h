@@ -139,13 +139,16 @@ int vae2_bn_eval_coeffs(const float* gamma, const float* beta,
                         const float* running_mean, const float* running_var,
                         float eps, int64_t c, float* save, void* stream);
 
-/* y = x*scale + shift (+ res) (then ReLU if relu).                             */
+/* y = fma(x, scale, shift) (+ res) (then ReLU if relu).  Only channels [0, c)
+ * of each pixel are written.                                                  */
 int vae2_bn_apply(const float* x, const vae2_act* xd, const float* save,
                   const float* res, const vae2_act* rd, float* y,
                   const vae2_act* yd, int relu, void* stream);
 
 /* Backward reduce: g = dy * (y > 0 if relu); partials [2][rows][c] of
- * (sum g, sum g*xhat), xhat = (x - mean)*invstd.                              */
+ * (sum g, sum g*xhat), xhat = (x - mean)*invstd.  With relu and y == NULL the
+ * mask is recomputed as fma(x, scale, shift) > 0 — exactly vae2_bn_apply's
+ * forward output when it had no residual — saving the read of y.              */
 int vae2_bn_relu_bwd_reduce(const float* dy, const vae2_act* dyd,
                             const float* y, const vae2_act* yd, const float* x,
                             const vae2_act* xd, const float* save, int relu,
@@ -156,7 +159,8 @@ int vae2_bn_bwd_param_grads(const double* sums, int64_t c, float* dgamma,
                             float* dbeta, void* stream);
 
 /* dx = gamma*invstd*(g - sum_g/count - xhat*sum_gxhat/count);
- * also dres = g when dres != NULL (residual branch of the block).             */
+ * also dres = g when dres != NULL (residual branch of the block).  The ReLU
+ * mask comes from y, or from x as in vae2_bn_relu_bwd_reduce when y == NULL. */
 int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
                            const vae2_act* yd, const float* x,
                            const vae2_act* xd, const float* save,

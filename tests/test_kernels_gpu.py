@@ -63,11 +63,17 @@ def test_conv_fwd_bwd(shape):
         assert rel(cg.bias.grad, conv.bias.grad) < TOL
 
 
-@pytest.mark.parametrize("relu,res,stride", [(True, False, 1), (False, False, 2), (True, True, 1)])
-def test_conv_bn_train(relu, res, stride):
+@pytest.mark.parametrize("relu,res,stride,cout", [
+    (True, False, 1, 36), (False, False, 2, 36), (True, True, 1, 36),
+    # channel-quad kernels: padded last quad (18 -> 20, 7 -> 8, 5 -> 8), wide (270: 68 quads)
+    (True, False, 1, 18), (True, True, 1, 18), (True, False, 1, 270), (True, True, 2, 5),
+    (True, True, 1, 7),
+    # residual as an unaligned channel slice: the scalar fallback
+    (True, "view", 1, 18)])
+def test_conv_bn_train(relu, res, stride, cout):
     from vae2 import ops
     torch.manual_seed(1)
-    n, h, w, cin, cout = 4, 12, 10, 18, 36
+    n, h, w, cin = 4, 12, 10, 18
     conv = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
     bn = nn.BatchNorm2d(cout, momentum=0.01)
     nn.init.normal_(bn.weight, 1.0, 0.2)
@@ -89,7 +95,12 @@ def test_conv_bn_train(relu, res, stride):
     gy = torch.randn_like(y_ref)
     y_ref.backward(gy)
     xg = nhwc(x.detach()).to(DEV).requires_grad_(True)
-    rg = nhwc(r.detach()).to(DEV).requires_grad_(True) if res else None
+    if res == "view":
+        wide = torch.zeros(n, oh, ow, cout + 3, device=DEV)
+        wide[..., 1:1 + cout] = nhwc(r.detach()).to(DEV)
+        rg = wide[..., 1:1 + cout].requires_grad_(True)
+    else:
+        rg = nhwc(r.detach()).to(DEV).requires_grad_(True) if res else None
     yg = ops.conv_bn(xg, conv_g, bn_g, relu=relu, residual=rg)
     yg.backward(nhwc(gy).to(DEV))
     torch.cuda.synchronize()

@@ -41,8 +41,8 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
     if (tid < S) {
       const int c = tid % C;
       const int rr = tid / C;
-      float mean = 0.f, invstd = 0.f;
-      if (MODE == 1) { mean = save[c]; invstd = save[C + c]; }
+      float mean = 0.f, invstd = 0.f, sc = 0.f, sh = 0.f;
+      if (MODE == 1) { mean = save[c]; invstd = save[C + c]; sc = save[2 * C + c]; sh = save[3 * C + c]; }
       for (int64_t p = p0 + rr; p < p1; p += R) {
         float v = x[p * xd.ps + c];
         if (MODE == 0) {
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
           s1 += v * v;
         } else {
           float gv = dy[p * dyd.ps + c];
-          if (relu && !(y[p * yd.ps + c] > 0.f)) gv = 0.f;
+          if (relu && !((y ? y[p * yd.ps + c] : __builtin_fmaf(v, sc, sh)) > 0.f)) gv = 0.f;
           s0 += gv;
           s1 += gv * (v - mean) * invstd;
         }
@@ -71,8 +71,8 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
   } else {
     for (int c = tid; c < C; c += 256) {
       float s0 = 0.f, s1 = 0.f;
-      float mean = 0.f, invstd = 0.f;
-      if (MODE == 1) { mean = save[c]; invstd = save[C + c]; }
+      float mean = 0.f, invstd = 0.f, sc = 0.f, sh = 0.f;
+      if (MODE == 1) { mean = save[c]; invstd = save[C + c]; sc = save[2 * C + c]; sh = save[3 * C + c]; }
       for (int64_t p = p0; p < p1; ++p) {
         float v = x[p * xd.ps + c];
         if (MODE == 0) {
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
           s1 += v * v;
         } else {
           float gv = dy[p * dyd.ps + c];
-          if (relu && !(y[p * yd.ps + c] > 0.f)) gv = 0.f;
+          if (relu && !((y ? y[p * yd.ps + c] : __builtin_fmaf(v, sc, sh)) > 0.f)) gv = 0.f;
           s0 += gv;
           s1 += gv * (v - mean) * invstd;
         }
@@ -88,6 +88,210 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
       part[(int64_t)blockIdx.x * C + c] = s0;
       part[((int64_t)rows + blockIdx.x) * C + c] = s1;
     }
+  }
+}
+
+// ------------------------------------------- channel-quad-stationary path ----
+// Thread (r, q) of a block owns channels 4q..4q+3 and walks pixels r, r+rows, ...
+// so per-channel coefficients stay in registers and every access is a 16-byte
+// load/store of a contiguous pixel run.  Needs pixel strides % 4 == 0, 16-byte
+// aligned bases and ceil(C/4) <= 256.  Channels >= C of the last quad are read
+// (pixel padding, discarded) but never written.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+__device__ __forceinline__ f4 chan4(const float* a, int c, int C) {
+  f4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = (c + k < C) ? a[c + k] : 0.f;
+  return v;
+}
+
+__device__ __forceinline__ void st4(float* p, f4 v, int c, int C) {
+  if (c + 4 <= C) {
+    *reinterpret_cast<f4*>(p) = v;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < C) p[k] = v[k];
+  }
+}
+
+static inline int quad_rows(int64_t C) { return 256 / (int)((C + 3) / 4); }
+constexpr int kApplyU = 4;  // pixels per thread in the apply kernels
+
+__global__ __launch_bounds__(256) void bn_apply_q_kernel(
+    const float* __restrict__ x, Act xd, const float* __restrict__ save,
+    const float* __restrict__ res, Act rd, float* __restrict__ y, Act yd, int relu,
+    int rows) {
+  const int C = (int)xd.c, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const f4 sc = chan4(save + 2 * C, c, C), sh = chan4(save + 3 * C, c, C);
+  const int64_t P = xd.n * xd.h * xd.w;
+  const int64_t pb = (int64_t)blockIdx.x * rows * kApplyU + r;
+  f4 v[kApplyU], rv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * rows;
+    if (p < P) {
+      v[u] = ld4(x + p * xd.ps + c);
+      if (res) rv[u] = ld4(res + p * rd.ps + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * rows;
+    if (p >= P) break;
+    f4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float t = __builtin_fmaf(v[u][k], sc[k], sh[k]);
+      if (res) t += rv[u][k];
+      o[k] = (relu && !(t > 0.f)) ? 0.f : t;
+    }
+    st4(y + p * yd.ps + c, o, c, C);
+  }
+}
+
+// Per-block partial rows: MODE 0 (sum x, sum x^2); MODE 1 (sum g, sum g*xhat) with
+// g = dy masked by the ReLU of the forward output (y, or recomputed from x).
+template <int MODE>
+__global__ __launch_bounds__(256) void chan_partials_q_kernel(
+    const float* __restrict__ x, Act xd, const float* __restrict__ dy, Act dyd,
+    const float* __restrict__ y, Act yd, const float* __restrict__ save, int relu,
+    int64_t ppb, int rows, float* __restrict__ part) {
+  __shared__ float red[2][256 * 4];
+  const int C = (int)xd.c, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  const int64_t P = xd.n * xd.h * xd.w;
+  const int64_t p0 = blockIdx.x * ppb;
+  int64_t p1 = p0 + ppb;
+  if (p1 > P) p1 = P;
+  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  if (tid < rows * c4) {
+    f4 mean = {0.f, 0.f, 0.f, 0.f}, invstd = mean, sc = mean, sh = mean;
+    if (MODE == 1) {
+      mean = chan4(save, c, C);
+      invstd = chan4(save + C, c, C);
+      sc = chan4(save + 2 * C, c, C);
+      sh = chan4(save + 3 * C, c, C);
+    }
+    int64_t p = p0 + r;
+    for (; p + rows < p1; p += 2 * rows) {  // two pixels in flight
+      const f4 xa = ld4(x + p * xd.ps + c), xb = ld4(x + (p + rows) * xd.ps + c);
+      if (MODE == 0) {
+        s0 += xa + xb;
+        s1 += xa * xa + xb * xb;
+      } else {
+        f4 ga = ld4(dy + p * dyd.ps + c), gb = ld4(dy + (p + rows) * dyd.ps + c);
+        f4 ya, yb;
+        if (relu && y) {
+          ya = ld4(y + p * yd.ps + c);
+          yb = ld4(y + (p + rows) * yd.ps + c);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (relu) {
+            const float ma = y ? ya[k] : __builtin_fmaf(xa[k], sc[k], sh[k]);
+            const float mb = y ? yb[k] : __builtin_fmaf(xb[k], sc[k], sh[k]);
+            if (!(ma > 0.f)) ga[k] = 0.f;
+            if (!(mb > 0.f)) gb[k] = 0.f;
+          }
+          s0[k] += ga[k] + gb[k];
+          s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k] + gb[k] * (xb[k] - mean[k]) * invstd[k];
+        }
+      }
+    }
+    if (p < p1) {
+      const f4 xa = ld4(x + p * xd.ps + c);
+      if (MODE == 0) {
+        s0 += xa;
+        s1 += xa * xa;
+      } else {
+        f4 ga = ld4(dy + p * dyd.ps + c);
+        f4 ya;
+        if (relu && y) ya = ld4(y + p * yd.ps + c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (relu && !((y ? ya[k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f)) ga[k] = 0.f;
+          s0[k] += ga[k];
+          s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+        }
+      }
+    }
+  }
+  // rows x (4*c4) layout: red[q][r * 4*c4 + c + k]
+  if (tid < rows * c4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[0][r * 4 * c4 + c + k] = s0[k];
+      red[1][r * 4 * c4 + c + k] = s1[k];
+    }
+  }
+  __syncthreads();
+  const int rowsC = (int)gridDim.x;
+  for (int ch = tid; ch < C; ch += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < rows; ++i) {
+      a += red[0][i * 4 * c4 + ch];
+      b += red[1][i * 4 * c4 + ch];
+    }
+    part[(int64_t)blockIdx.x * C + ch] = a;
+    part[((int64_t)rowsC + blockIdx.x) * C + ch] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_q_kernel(
+    const float* __restrict__ dy, Act dyd, const float* __restrict__ y, Act yd,
+    const float* __restrict__ x, Act xd, const float* __restrict__ save,
+    const float* __restrict__ gamma, const double* __restrict__ sums, double count,
+    int relu, float* __restrict__ dx, Act dxd, float* __restrict__ dres, Act rd, int rows) {
+  const int C = (int)xd.c, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const float inv_n = (float)(1.0 / count);
+  f4 mean, invstd, sc, sh, mg, mgx, k4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = c + k < C ? c + k : C - 1;
+    mean[k] = save[ch];
+    invstd[k] = save[C + ch];
+    sc[k] = save[2 * C + ch];
+    sh[k] = save[3 * C + ch];
+    mg[k] = (float)sums[ch] * inv_n;
+    mgx[k] = (float)sums[C + ch] * inv_n;
+    k4[k] = (gamma ? gamma[ch] : 1.f) * invstd[k];
+  }
+  const int64_t P = xd.n * xd.h * xd.w;
+  const int64_t pb = (int64_t)blockIdx.x * rows * kApplyU + r;
+  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * rows;
+    if (p < P) {
+      gv[u] = ld4(dy + p * dyd.ps + c);
+      xv[u] = ld4(x + p * xd.ps + c);
+      if (relu && y) yv[u] = ld4(y + p * yd.ps + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * rows;
+    if (p >= P) break;
+    f4 g = gv[u], o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (relu && !((y ? yv[u][k] : __builtin_fmaf(xv[u][k], sc[k], sh[k])) > 0.f)) g[k] = 0.f;
+      const float xh = (xv[u][k] - mean[k]) * invstd[k];
+      o[k] = k4[k] * (g[k] - mg[k] - xh * mgx[k]);
+    }
+    if (dres) st4(dres + p * rd.ps + c, g, c, C);
+    st4(dx + p * dxd.ps + c, o, c, C);
   }
 }
 
@@ -228,7 +432,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
        i += gridDim.x * blockDim.x) {
     uint32_t p = cdiv.div(i);
     uint32_t c = i - p * C;
-    float v = x[(int64_t)p * xd.ps + c] * scale[c] + shift[c];
+    float v = __builtin_fmaf(x[(int64_t)p * xd.ps + c], scale[c], shift[c]);
     if (res) v += res[(int64_t)p * rd.ps + c];
     if (relu) v = v > 0.f ? v : 0.f;
     y[(int64_t)p * yd.ps + c] = v;
@@ -253,7 +457,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel_v4(
     f4 v = *reinterpret_cast<const f4*>(x + (int64_t)p * xd.ps + c);
     f4 sc = *reinterpret_cast<const f4*>(scale + c);
     f4 sh = *reinterpret_cast<const f4*>(shift + c);
-    v = v * sc + sh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_fmaf(v[k], sc[k], sh[k]);
     if (res) v += *reinterpret_cast<const f4*>(res + (int64_t)p * rd.ps + c);
     if (relu) {
 #pragma unroll
@@ -277,13 +482,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     uint32_t p = cdiv.div(i);
     uint32_t c = i - p * C;
     float g = dy[(int64_t)p * dyd.ps + c];
-    if (relu && !(y[(int64_t)p * yd.ps + c] > 0.f)) g = 0.f;
+    const float xv = x[(int64_t)p * xd.ps + c];
+    if (relu && !((y ? y[(int64_t)p * yd.ps + c]
+                     : __builtin_fmaf(xv, save[2 * C + c], save[3 * C + c])) > 0.f))
+      g = 0.f;
     if (dres) dres[(int64_t)p * rd.ps + c] = g;
     float mean = save[c], invstd = save[C + c];
     float mg = (float)sums[c] * inv_n;
     float mgx = (float)sums[C + c] * inv_n;
     float gm = gamma ? gamma[c] : 1.f;
-    float xh = (x[(int64_t)p * xd.ps + c] - mean) * invstd;
+    float xh = (xv - mean) * invstd;
     dx[(int64_t)p * dxd.ps + c] = gm * invstd * (g - mg - xh * mgx);
   }
 }
@@ -316,6 +524,8 @@ static bool v4_ok(const void* p, int64_t ps) {
   return ((uintptr_t)p % 16 == 0) && (ps % 4 == 0);
 }
 
+static bool quad_ok(int64_t c) { return (c + 3) / 4 <= 256; }
+
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream) {
   hipLaunchKernelGGL(colsum_to_float_kernel, dim3((unsigned)c), dim3(256), 0,
@@ -341,6 +551,13 @@ int vae2_bn_stats(const float* x, const vae2_act* xd, float* partials,
   int64_t P = act_pixels(xd);
   int64_t ppb = pix_per_block(P);
   Act a = to_act(xd);
+  if (quad_ok(xd->c) && v4_ok(x, xd->ps)) {
+    hipLaunchKernelGGL((chan_partials_q_kernel<0>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
+                       0, as_stream(stream), x, a, (const float*)nullptr, a,
+                       (const float*)nullptr, a, (const float*)nullptr, 0, ppb,
+                       quad_rows(xd->c), partials);
+    return check_launch(fn);
+  }
   hipLaunchKernelGGL((chan_partials_kernel<0>), dim3((unsigned)ceil_div(P, ppb)),
                      dim3(256), 0, as_stream(stream), x, a, (const float*)nullptr, a,
                      (const float*)nullptr, a, (const float*)nullptr, 0, ppb, partials);
@@ -422,6 +639,14 @@ int vae2_bn_apply(const float* x, const vae2_act* xd, const float* save,
   }
   int64_t total = act_elems(xd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
+  if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(y, yd->ps) && (!res || v4_ok(res, rd->ps))) {
+    const int rows = quad_rows(xd->c);
+    hipLaunchKernelGGL(bn_apply_q_kernel,
+                       dim3((unsigned)ceil_div(act_pixels(xd), (int64_t)rows * kApplyU)),
+                       dim3(256), 0, as_stream(stream), x, to_act(xd), save, res, r, y,
+                       to_act(yd), relu, rows);
+    return check_launch(fn);
+  }
   bool vec = (xd->c % 4 == 0) && v4_ok(x, xd->ps) && v4_ok(y, yd->ps) &&
              (!res || v4_ok(res, rd->ps)) && v4_ok(save, 4);
   if (vec) {
@@ -442,10 +667,17 @@ int vae2_bn_relu_bwd_reduce(const float* dy, const vae2_act* dyd,
                             float* partials, void* stream) {
   const char* fn = "vae2_bn_relu_bwd_reduce";
   VAE2_REQUIRE(dy && x && save && partials && act_ok(dyd) && act_ok(xd), fn, "bad arguments");
-  VAE2_REQUIRE(!relu || (y && act_ok(yd)), fn, "relu needs y");
+  VAE2_REQUIRE(!y || act_ok(yd), fn, "bad y descriptor");
   int64_t P = act_pixels(xd);
   int64_t ppb = pix_per_block(P);
-  Act ya = relu ? to_act(yd) : to_act(xd);
+  Act ya = (relu && y) ? to_act(yd) : to_act(xd);
+  if (!relu) y = nullptr;
+  if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(dy, dyd->ps) && (!y || v4_ok(y, yd->ps))) {
+    hipLaunchKernelGGL((chan_partials_q_kernel<1>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
+                       0, as_stream(stream), x, to_act(xd), dy, to_act(dyd), y, ya, save, relu,
+                       ppb, quad_rows(xd->c), partials);
+    return check_launch(fn);
+  }
   hipLaunchKernelGGL((chan_partials_kernel<1>), dim3((unsigned)ceil_div(P, ppb)),
                      dim3(256), 0, as_stream(stream), x, to_act(xd), dy, to_act(dyd), y,
                      ya, save, relu, ppb, partials);
@@ -470,11 +702,22 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
   const char* fn = "vae2_bn_relu_bwd_apply";
   VAE2_REQUIRE(dy && x && save && sums && dx && act_ok(dyd) && act_ok(xd) && act_ok(dxd),
                fn, "bad arguments");
-  VAE2_REQUIRE(!relu || (y && act_ok(yd)), fn, "relu needs y");
+  VAE2_REQUIRE(!y || act_ok(yd), fn, "bad y descriptor");
   VAE2_REQUIRE(!dres || act_ok(dresd), fn, "bad dres descriptor");
   int64_t total = act_elems(xd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
-  Act ya = relu ? to_act(yd) : to_act(xd);
+  Act ya = (relu && y) ? to_act(yd) : to_act(xd);
+  if (!relu) y = nullptr;
+  if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(dy, dyd->ps) && v4_ok(dx, dxd->ps) &&
+      (!y || v4_ok(y, yd->ps)) && (!dres || v4_ok(dres, dresd->ps))) {
+    const int rows = quad_rows(xd->c);
+    hipLaunchKernelGGL(bn_bwd_apply_q_kernel,
+                       dim3((unsigned)ceil_div(act_pixels(xd), (int64_t)rows * kApplyU)),
+                       dim3(256), 0, as_stream(stream), dy, to_act(dyd), y, ya, x, to_act(xd),
+                       save, gamma, sums, count, relu, dx, to_act(dxd), dres,
+                       dres ? to_act(dresd) : to_act(xd), rows);
+    return check_launch(fn);
+  }
   Act ra = dres ? to_act(dresd) : to_act(xd);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), dy, to_act(dyd), y, ya, x, to_act(xd), save, gamma,

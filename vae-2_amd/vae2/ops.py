@@ -329,6 +329,8 @@ class _ConvBN(torch.autograd.Function):
         dyp, dya = act_of(dy)
         rp, ra = act_of(r)
         yp, ya = act_of(y)
+        if not ctx.has_res:
+            yp = None  # the kernels recompute the ReLU mask from r (no read of y)
         rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
         part = _empty((2 * rows * cout,), r)
         call("vae2_bn_relu_bwd_reduce", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
