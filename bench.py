@@ -185,7 +185,8 @@ def main():
 
     # ---- roofline phase: the same step, the dominant kernel's launches timed with
     # HIP events on their stream, each launch isolated from the side streams ----
-    kname = prof.fwd_kernel_name(B, H, W, 64)
+    from vae2 import _lib
+    kname = prof.fwd_kernel_name(_lib.Act(B, H, W, 64, 64), (B, H, W, 64), 3, 1, 1)
     timer = prof.KernelTimer(kname)
     if not args.no_roofline and args.roofline_steps > 0:
         torch.cuda.synchronize()

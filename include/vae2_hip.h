@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 1
+#define VAE2_ABI_VERSION 2
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -40,9 +40,17 @@ const char* vae2_last_error(void);
 /* ---------------------------------------------------------------- conv ---- */
 
 /* Rows of BN partial statistics that vae2_conv2d_fwd writes when stats != NULL
- * (one row of `cout` sums and one of `cout` sums of squares per row).
+ * (one row of `cout` sums and one of `cout` sums of squares per row), for this
+ * input (its address decides which kernel runs), geometry and output.
  * Workspace = 2 * rows * cout floats.                                         */
-int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout);
+int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae2_act* yd,
+                                   int k, int stride, int pad);
+
+/* Conv algorithm selection (tuning / A-B measurement): 0 = auto, 1 = the gather
+ * implicit-GEMM kernel only, 2 = the LDS-tiled direct 3x3 kernel wherever legal
+ * (k = 3, stride 1, pad 1, 16-byte aligned input with ps % 4 == 0).  Returns the
+ * previous setting.  Process-wide; set it before building stats buffers.        */
+int vae2_conv2d_set_algo(int algo);
 
 /* Conv weights are consumed in a packed layout (zero-padded, K = (tap, 4-channel
  * quad) ordered): mode 0 for vae2_conv2d_fwd  = [round_up(Cout,64)][k*k][round_up(Cin,4)],
@@ -72,10 +80,10 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
                     int stride, int pad, float beta, float* stats,
                     void* stream);
 
-/* Name of the kernel instantiation a vae2_conv2d_fwd launch with this output
- * uses (e.g. "igemm_kernel<2, 4, 0>"), for matching timings with rocprof.     */
-int vae2_conv2d_fwd_kernel_name(const vae2_act* yd, int64_t cout, char* buf,
-                                int64_t len);
+/* Name of the kernel instantiation a vae2_conv2d_fwd launch with this geometry
+ * uses (e.g. "igemm_kernel<4, 4, true, 0>"), for matching timings with rocprof. */
+int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, int stride,
+                                int pad, char* buf, int64_t len);
 
 /* dx = conv2d_transpose(dy, w) (+ beta*dx) with w packed (mode 1): gradient of
  * vae2_conv2d_fwd w.r.t. its input (autograd's convolution_backward, input half). */

@@ -63,6 +63,84 @@ def test_conv_fwd_bwd(shape):
         assert rel(cg.bias.grad, conv.bias.grad) < TOL
 
 
+DIRECT_SHAPES = [
+    # N, H, W, Cin, Cout, bias: 3x3 / stride 1 / pad 1 through the LDS-tiled kernel
+    (2, 16, 32, 18, 18, False),   # one slab (5 quads), padded channel quad
+    (2, 13, 40, 36, 36, True),    # partial row and column tiles, 2 slabs
+    (1, 8, 64, 64, 64, False),    # 2 slabs of 8 quads, TN = 4
+    (2, 5, 7, 3, 5, False),       # image smaller than one tile, TM = 2
+    (1, 8, 32, 154, 144, False),  # 5 slabs (39 quads), N split over 3 blocks
+    (2, 6, 33, 256, 18, True),    # 8 slabs, 2 column tiles of which one has 1 column
+]
+
+
+@pytest.mark.parametrize("shape", DIRECT_SHAPES)
+def test_direct_conv3x3(shape):
+    from vae2 import _lib, ops
+    torch.manual_seed(3)
+    n, h, w, cin, cout, bias = shape
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias)
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    y_ref = conv(x)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    cg = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    lib = _lib.load()
+    prev = lib.vae2_conv2d_set_algo(2)
+    try:
+        xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+        with torch.no_grad():
+            xg.copy_(nhwc(x.detach()).to(DEV))
+        xg.requires_grad_(True)
+        dyg = ops.new_act((n, h, w, cout), xg)
+        with torch.no_grad():
+            dyg.copy_(nhwc(gy).to(DEV))
+        yg = ops.conv(xg, cg)
+        yg.backward(dyg)
+        torch.cuda.synchronize()
+        name = ctypes_name(xg, (n, h, w, cout))
+        assert name.startswith("dconv3_kernel"), name
+    finally:
+        lib.vae2_conv2d_set_algo(prev)
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(nchw(xg.grad), x.grad) < TOL
+    assert rel(cg.weight.grad, conv.weight.grad) < TOL
+    if bias:
+        assert rel(cg.bias.grad, conv.bias.grad) < TOL
+
+
+def ctypes_name(x, yshape):
+    from vae2 import ops, prof
+    _, xa = ops.act_of(x)
+    return prof.fwd_kernel_name(xa, yshape, 3, 1, 1)
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(18, 18, 16, 32), (64, 36, 12, 40)])
+def test_direct_conv3x3_bn_stats(cin, cout, h, w):
+    """BN statistics from the direct kernel's epilogue (its own partial-row count)."""
+    from vae2 import _lib, ops
+    torch.manual_seed(4)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    bn = nn.BatchNorm2d(cout, momentum=0.01)
+    x = torch.randn(2, cin, h, w)
+    y_ref = F.relu(bn(conv(x)))
+    cg, bg = nn.Conv2d(cin, cout, 3, 1, 1, bias=False).to(DEV), nn.BatchNorm2d(cout, momentum=0.01).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    lib = _lib.load()
+    prev = lib.vae2_conv2d_set_algo(2)
+    try:
+        xg = ops.new_act((2, h, w, cin), torch.empty(1, device=DEV))
+        xg.copy_(nhwc(x).to(DEV))
+        yg = ops.conv_bn(xg, cg, bg, relu=True)
+        torch.cuda.synchronize()
+    finally:
+        lib.vae2_conv2d_set_algo(prev)
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(bg.running_mean, bn.running_mean) < 1e-5
+    assert rel(bg.running_var, bn.running_var) < 1e-5
+
+
 @pytest.mark.parametrize("relu,res,stride,cout", [
     (True, False, 1, 36), (False, False, 2, 36), (True, True, 1, 36),
     # channel-quad kernels: padded last quad (18 -> 20, 7 -> 8, 5 -> 8), wide (270: 68 quads)

@@ -290,6 +290,184 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
   }
 }
 
+// ------------------------------------------------------ direct 3x3 (LDS) ----
+// 3x3 / stride-1 / pad-1 convolutions (the HRNet branch convs) — forward, and the
+// data gradient with flipped taps and mode-1 weights.  A workgroup owns an output
+// tile of (2*TM) rows x 32 columns of one image; per slab of <= 32 input channels it
+// stages the (2*TM+2) x 34 halo tile in LDS once (zero halo, zero channel padding),
+// then builds every tap's A fragment from LDS with one ds_read_b128 per lane.  The
+// gather kernel re-reads each input element once per tap through L1/L2; here it is
+// read once (+ halo).  K order inside a slab is (tap, quad), lane group g taking quad
+// 4c+g of chunk c (as igemm_kernel), so B comes from the same packed weights.
+struct DConv {
+  const float* a;
+  int a_ps, a_c, a_c4, img_h, img_w;
+  int tiles_h, tiles_w;  // output tiles per image
+  int cs4;               // channel quads per slab
+  const float* w;        // packed [Npad][9][a_c4]
+  uint32_t a_bytes, w_bytes;
+  int n;
+  const float* bias;
+  float* y;
+  int y_ps;
+  float beta;
+  float* stats;  // [2][gridDim.x][n] or null
+};
+
+constexpr int kDcBW = 32;     // tile columns
+constexpr int kDcMaxCs4 = 8;  // quads per slab
+
+template <int TM, int TN, bool FLIP>
+__global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
+  constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
+  constexpr int BN = 16 * TN;
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  __shared__ float red[4][2][BN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int bm = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_img = p.tiles_h * p.tiles_w;
+  const int img = bm / per_img;
+  const int trem = bm - img * per_img;
+  const int th = trem / p.tiles_w;
+  const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * kDcBW;
+  const int n0 = blockIdx.y * BN;
+  const int kk4 = 9 * p.a_c4;
+  const int csp = p.cs4 * 4 + 4;  // LDS floats per pixel (+4: bank spread)
+  const int Q = p.a_c4 >> 2;
+
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int trow = wave * (TM / 2) + (i >> 1), tcol = (i & 1) * 16 + r;
+    abase[i] = ((trow + 1) * LW + tcol + 1) * csp;
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(p.w, p.w_bytes);
+  uint32_t wrow[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) wrow[j] = (uint32_t)((n0 + j * 16 + r) * kk4) * 4u;
+
+  f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const f4* fa, const f4* fb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  const int img_base = img * p.img_h;
+  for (int q0 = 0; q0 < Q; q0 += p.cs4) {
+    const int qs = Q - q0 < p.cs4 ? Q - q0 : p.cs4;
+    // ---- stage the halo tile of this slab (zero outside the image / past a_c) ----
+    __syncthreads();
+    const int total = LH * LW * qs;
+    for (int i = threadIdx.x; i < total; i += 256) {
+      const int pix = i / qs;
+      const int q = i - pix * qs;
+      const int lr = pix / LW, lc = pix - lr * LW;
+      const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+      const bool ok = (unsigned)ih < (unsigned)p.img_h && (unsigned)iw < (unsigned)p.img_w;
+      const int c = (q0 + q) * 4;
+      const uint32_t off =
+          ok ? (uint32_t)(((img_base + ih) * p.img_w + iw) * p.a_ps + c) * 4u : kOOB;
+      f4 v = load4(arsrc, off);
+      if (c + 4 > p.a_c) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c + k >= p.a_c) v[k] = 0.f;
+      }
+      *reinterpret_cast<f4*>(&tile[pix * csp + 4 * q]) = v;
+    }
+    __syncthreads();
+    // ---- 9 taps x qs quads of K from LDS ----
+    const int nch = (9 * qs + 3) >> 2;
+    int t = 0, q = g;
+    while (q >= qs) { q -= qs; ++t; }
+    auto load = [&](f4* fa, f4* fb) {
+      const bool tv = t < 9;
+      const int tt = tv ? t : 0;
+      const int dh = (tt >= 3) + (tt >= 6) - 1;
+      const int dw = tt - 3 * (dh + 1) - 1;
+      const int aoff = (dh * LW + dw) * csp + 4 * q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const f4*>(&tile[abase[i] + aoff]);
+      const int tl = FLIP ? 8 - tt : tt;
+      const uint32_t woff = tv ? (uint32_t)(tl * p.a_c4 + (q0 + q) * 4) * 4u : kOOB;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
+      q += 4;
+      while (q >= qs) { q -= qs; ++t; }
+    };
+    load(fa0, fb0);
+    for (int ch = 0; ch < nch; ch += 2) {
+      load(fa1, fb1);
+      mma(fa0, fb0);
+      load(fa0, fb0);
+      mma(fa1, fb1);
+    }
+  }
+
+  // ---- epilogue (bias, beta*y, BN partial statistics) ----
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int oh = oh0 + wave * (TM / 2) + (i >> 1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
+      if (oh >= p.img_h || ow >= p.img_w) continue;
+      float* yrow = p.y + (int64_t)((img_base + oh) * p.img_w + ow) * p.y_ps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 16 + r;
+        if (n >= p.n) continue;
+        float v = acc[i][j][e];
+        if (p.bias) v += p.bias[n];
+        if (p.beta != 0.f) v += p.beta * yrow[n];
+        yrow[n] = v;
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] += __shfl_xor(csum[j], 16, 64);
+      csum[j] += __shfl_xor(csum[j], 32, 64);
+      csq[j] += __shfl_xor(csq[j], 16, 64);
+      csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        red[wave][0][j * 16 + r] = csum[j];
+        red[wave][1][j * 16 + r] = csq[j];
+      }
+    }
+    __syncthreads();
+    const int rows = gridDim.x;
+    for (int c = threadIdx.x; c < BN; c += 256) {
+      if (n0 + c >= p.n) continue;
+      float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+      p.stats[bm * p.n + n0 + c] = s;
+      p.stats[(rows + bm) * p.n + n0 + c] = s2;
+    }
+  }
+}
+
 // ------------------------------------------------------------ tiling ----
 struct Tile {
   int tm, tn, nblk;
@@ -579,6 +757,83 @@ static uint32_t act_bytes(const vae2_act* d) {
 
 using namespace vae2;
 
+// ---------------------------------------------- direct 3x3: host dispatch ----
+static int g_conv_algo = 0;  // 0 auto, 1 gather kernel only, 2 direct wherever legal
+
+struct DTile {
+  int tm, tn, nblk, cs4, tiles_h, tiles_w;
+};
+
+static bool dconv_legal(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
+                        const float* a) {
+  return k == 3 && stride == 1 && pad == 1 && ad->h == yd->h && ad->w == yd->w &&
+         vec_ok(a, (int)ad->ps);
+}
+
+static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd) {
+  DTile d;
+  Tile t = pick_tile(act_pixels(yd), (int)yd->c);
+  d.tn = t.tn;
+  d.nblk = t.nblk;
+  const int Q = round_up((int)ad->c, 4) / 4;
+  const int nsl = (Q + kDcMaxCs4 - 1) / kDcMaxCs4;
+  d.cs4 = (Q + nsl - 1) / nsl;  // balanced slabs
+  d.tiles_w = (int)ceil_div(yd->w, kDcBW);
+  // 8-row tiles unless that leaves fewer than ~3 workgroups per CU
+  d.tm = 4;
+  if (yd->h < 8 || ad->n * ceil_div(yd->h, 8) * d.tiles_w * d.nblk < 768) d.tm = 2;
+  d.tiles_h = (int)ceil_div(yd->h, 2 * d.tm);
+  return d;
+}
+
+static bool dconv_use(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
+                      const float* a) {
+  if (g_conv_algo == 1 || !dconv_legal(ad, yd, k, stride, pad, a)) return false;
+  if (g_conv_algo == 2) return true;
+  // auto: enough workgroups to fill the chip (narrow images waste partial 32-column
+  // tiles and low-resolution layers have too few tiles: the gather kernel wins there)
+  DTile d = pick_dtile(ad, yd);
+  return ad->w >= 16 && ad->n * d.tiles_h * d.tiles_w * d.nblk >= 256;
+}
+
+template <int TM, bool FLIP>
+static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
+  switch (tn) {
+#define CASE(T) \
+  case T: hipLaunchKernelGGL((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p); break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+  }
+}
+
+static int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                        const float* bias, float* y, const vae2_act* yd, float beta,
+                        float* stats, bool flip, hipStream_t s, const char* fn) {
+  DTile d = pick_dtile(ad, yd);
+  DConv p{};
+  p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
+  p.img_h = (int)ad->h; p.img_w = (int)ad->w;
+  p.tiles_h = d.tiles_h; p.tiles_w = d.tiles_w; p.cs4 = d.cs4;
+  p.w = wp; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
+  p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
+  p.stats = stats;
+  dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
+  const size_t shm = (size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) * sizeof(float);
+  if (d.tm == 4) {
+    if (flip) dconv_launch_tn<4, true>(p, d.tn, grid, shm, s);
+    else dconv_launch_tn<4, false>(p, d.tn, grid, shm, s);
+  } else {
+    if (flip) dconv_launch_tn<2, true>(p, d.tn, grid, shm, s);
+    else dconv_launch_tn<2, false>(p, d.tn, grid, shm, s);
+  }
+  return check_launch(fn);
+}
+
+static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
+  DTile d = pick_dtile(ad, yd);
+  return ad->n * d.tiles_h * d.tiles_w;
+}
+
 extern "C" {
 
 int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode) {
@@ -606,13 +861,28 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
   return check_launch(fn);
 }
 
-int64_t vae2_conv2d_fwd_stats_rows(const vae2_act* yd, int64_t cout) {
-  return igemm_rows(act_pixels(yd), (int)cout);
+int vae2_conv2d_set_algo(int algo) {
+  const int prev = g_conv_algo;
+  if (algo >= 0 && algo <= 2) g_conv_algo = algo;
+  return prev;
 }
 
-int vae2_conv2d_fwd_kernel_name(const vae2_act* yd, int64_t cout, char* buf, int64_t len) {
-  if (!yd || !buf || len <= 0) return -22;
-  Tile t = pick_tile(act_pixels(yd), (int)cout);
+int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae2_act* yd,
+                                   int k, int stride, int pad) {
+  if (!act_ok(xd) || !act_ok(yd)) return 0;
+  if (dconv_use(xd, yd, k, stride, pad, x)) return dconv_rows(xd, yd);
+  return igemm_rows(act_pixels(yd), (int)yd->c);
+}
+
+int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, int stride,
+                                int pad, char* buf, int64_t len) {
+  if (!xd || !yd || !buf || len <= 0) return -22;
+  if (dconv_use(xd, yd, k, stride, pad, (const float*)16)) {
+    DTile d = pick_dtile(xd, yd);
+    snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
+    return 0;
+  }
+  Tile t = pick_tile(act_pixels(yd), (int)yd->c);
   snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0>", t.tm, t.tn);
   return 0;
 }
@@ -625,6 +895,10 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
   VAE2_REQUIRE(x && wp && y, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(xd, yd, k, stride, pad), fn, "inconsistent conv shapes");
   VAE2_REQUIRE(fits32(xd) && fits32(yd), fn, "tensor too large for 32-bit indexing");
+  if (dconv_use(xd, yd, k, stride, pad, x)) {
+    return launch_dconv(x, xd, wp, (uint32_t)(vae2_conv2d_packed_size(yd->c, xd->c, k, 0) * 4),
+                        bias, y, yd, beta, stats, false, as_stream(stream), fn);
+  }
   IGemm p{};
   p.a = x; p.a_ps = (int)xd->ps; p.a_c = (int)xd->c; p.a_c4 = round_up((int)xd->c, 4);
   p.a_h = (int)xd->h; p.a_w = (int)xd->w;
@@ -651,6 +925,9 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
   VAE2_REQUIRE(dy && wp && dx, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(dxd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
   VAE2_REQUIRE(fits32(dxd) && fits32(dyd), fn, "tensor too large for 32-bit indexing");
+  if (dconv_use(dyd, dxd, k, stride, pad, dy))
+    return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
+                        nullptr, dx, dxd, beta, nullptr, true, as_stream(stream), fn);
   // One launch per (ph, pw) stride-parity class of the input pixels: input row
   // ih = stride*i + ph receives from output row oh = (ih + pad - kh)/stride for every
   // kh with (ph + pad - kh) % stride == 0.

@@ -49,13 +49,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", type=int, nargs="*", help="indices into SHAPES")
+    ap.add_argument("--algo", type=int, nargs="*", default=[0],
+                    help="vae2_conv2d_set_algo values to compare (0 auto, 1 gather, 2 direct)")
     a = ap.parse_args()
     lib = _lib.load()
+    for algo in a.algo:
+        lib.vae2_conv2d_set_algo(algo)
+        print(f"== algo {algo}")
+        run(a, lib)
+
+
+def run(a, lib):
     dev = "cuda"
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'shape':34s} {'fwd us':>8s} {'TF/s':>6s} {'dgrad us':>9s} {'TF/s':>6s} "
           f"{'wgrad us':>9s} {'TF/s':>6s}")
-    for H, W, ci, co, k, st, cnt in SHAPES:
+    for idx, (H, W, ci, co, k, st, cnt) in enumerate(SHAPES):
+        if a.only and idx not in a.only:
+            continue
         B = a.batch
         x = ops.new_act((B, H, W, ci), torch.empty(1, device=dev))
         x.normal_()

@@ -34,10 +34,12 @@ _SIGS = {
     "vae2_conv2d_packed_size": (c_i64, [c_i64, c_i64, c_int, c_int]),
     "vae2_conv2d_pack_weight": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp]),
     "vae2_conv2d_pack_weights": (c_int, [c_vp, c_i64, c_vp]),
-    "vae2_conv2d_fwd_stats_rows": (c_i64, [P_ACT, c_i64]),
+    "vae2_conv2d_fwd_stats_rows": (c_i64, [c_vp, P_ACT, P_ACT, c_int, c_int, c_int]),
+    "vae2_conv2d_set_algo": (c_int, [c_int]),
     "vae2_conv2d_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                 c_f32, c_vp, c_vp]),
-    "vae2_conv2d_fwd_kernel_name": (c_int, [P_ACT, c_i64, ctypes.c_char_p, c_i64]),
+    "vae2_conv2d_fwd_kernel_name": (c_int, [P_ACT, P_ACT, c_int, c_int, c_int, ctypes.c_char_p,
+                                            c_i64]),
     "vae2_conv2d_bwd_data": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                      c_f32, c_vp]),
     "vae2_conv2d_bwd_weight_ws_size": (c_i64, [P_ACT, P_ACT, c_int]),
@@ -88,7 +90,7 @@ _SIGS = {
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

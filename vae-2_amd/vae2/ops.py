@@ -220,7 +220,7 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     yp, ya = act_of(y)
     timer = prof.active()
     ev = None
-    if timer is not None and timer.matches(n, oh, ow, cout):
+    if timer is not None and timer.matches(xa, (n, oh, ow, cout), spec):
         # algorithmic: 2*M*N*K flops; bytes = input read once + output written once + weights
         ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k,
                           4.0 * (n * h * w * xa.c + n * oh * ow * cout +
@@ -270,7 +270,10 @@ class _ConvBN(torch.autograd.Function):
         count = float(n * oh * ow)
         group = None
         if spec.training:
-            rows = lib.vae2_conv2d_fwd_stats_rows(ctypes.byref(Act(n, oh, ow, cout, cout)), cout)
+            xp, xa = act_of(x)
+            rows = lib.vae2_conv2d_fwd_stats_rows(xp, ctypes.byref(xa),
+                                                  ctypes.byref(Act(n, oh, ow, cout, cout)),
+                                                  spec.k, spec.stride, spec.pad)
             stats = _empty((2 * rows * cout,), x)
             r = _conv_fwd(x, weight, bias, spec, stats)
             sums = _empty((2 * cout,), x, torch.float64)

@@ -18,10 +18,14 @@ def active():
     return _ACTIVE
 
 
-def fwd_kernel_name(n, oh, ow, cout):
+def fwd_kernel_name(xa, yshape, k, stride, pad):
+    """Kernel instantiation vae2_conv2d_fwd uses for input act `xa` (aligned) and
+    output shape (n, oh, ow, cout)."""
     buf = ctypes.create_string_buffer(64)
-    a = _lib.Act(n, oh, ow, cout, cout)
-    _lib.check(_lib.load().vae2_conv2d_fwd_kernel_name(ctypes.byref(a), cout, buf, 64))
+    n, oh, ow, cout = yshape
+    y = _lib.Act(n, oh, ow, cout, cout)
+    _lib.check(_lib.load().vae2_conv2d_fwd_kernel_name(ctypes.byref(xa), ctypes.byref(y), k,
+                                                       stride, pad, buf, 64))
     return buf.value.decode()
 
 
@@ -45,10 +49,10 @@ class KernelTimer:
         _ACTIVE = None
         self.enabled = False
 
-    def matches(self, n, oh, ow, cout):
-        key = (n, oh, ow, cout)
+    def matches(self, xa, yshape, spec):
+        key = (xa.n, xa.h, xa.w, xa.c, xa.ps, yshape, spec.k, spec.stride, spec.pad)
         if key not in self._names:
-            self._names[key] = fwd_kernel_name(n, oh, ow, cout)
+            self._names[key] = fwd_kernel_name(xa, yshape, spec.k, spec.stride, spec.pad)
         return self._names[key] == self.kernel_name
 
     def record(self, flops, nbytes=0.0):
