@@ -660,6 +660,210 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
     }
 }
 
+// --------------------------------------------------- direct 3x3 wgrad (LDS) ----
+// dW of 3x3 / stride-1 / pad-1 convs.  A workgroup owns a (co slab, ci slab) of dW
+// and a run of BH x 32 pixel tiles; per tile it stages dY (transposed: [co][px]) and
+// the X halo tile (transposed: [ci][halo px]) in LDS once, then every wave sweeps all
+// the tile's pixels (MFMA k) for its own TN column tiles (columns = (tap, ci) of the
+// slab), so no cross-wave reduction is needed.  Partial slabs part[split][co][(t,ci)]
+// are summed by wgrad_reduce_kernel in a fixed order (deterministic).
+struct WGrad3 {
+  const float* x;
+  int x_ps, cin, cin4, h, w;
+  const float* dy;
+  int dy_ps, cout;
+  int tiles_h, tiles_w, ntiles, tiles_per_split;
+  int csw, n_ci_slabs;  // channels per ci slab (multiple of 4), slabs
+  uint32_t x_bytes, dy_bytes;
+  float* part;  // [splits][cout][9*cin4]
+};
+
+template <int TM, int TN, int BH, bool PF>
+__global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
+  constexpr int LH = BH + 2, LW = 34, NPX = BH * 32, LPX = LH * LW;
+  constexpr int DYS = NPX + 4;  // dY^T row stride (floats)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dyt = sm;                  // [16*TM][DYS]
+  float* xt = sm + 16 * TM * DYS;   // [csw + 1][LPX], row csw = zeros
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int cis = blockIdx.y % p.n_ci_slabs, cos = blockIdx.y / p.n_ci_slabs;
+  const int co0 = cos * 16 * TM, c0 = cis * p.csw;
+  const int csw_real = p.cin4 - c0 < p.csw ? p.cin4 - c0 : p.csw;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
+
+  int bbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = (wave * TN + j) * 16 + r;
+    const int t = n / p.csw;
+    const int cl = n - t * p.csw;
+    const bool ok = t < 9 && cl < csw_real;
+    bbase[j] = ok ? cl * LPX + (t / 3) * LW + (t % 3) : p.csw * LPX;
+  }
+  for (int i = threadIdx.x; i < LPX; i += 256) xt[p.csw * LPX + i] = 0.f;
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int per_img = p.tiles_h * p.tiles_w;
+  const int tb = blockIdx.x * p.tiles_per_split;
+  const int te = tb + p.tiles_per_split < p.ntiles ? tb + p.tiles_per_split : p.ntiles;
+  // Register prefetch: tile t+1's global loads are in flight while tile t computes.
+  constexpr int NI = NPX * 4 * TM / 256;     // dY items per thread
+  constexpr int NX = (LPX * 9 + 255) / 256;  // X items per thread (<= 9 quads per slab)
+  const int xtotal = LPX * (csw_real >> 2);
+  f4 pdy[NI], pxx[NX];
+  auto fetch = [&](int tile) {
+    const int img = tile / per_img;
+    const int trem = tile - img * per_img;
+    const int th = trem / p.tiles_w;
+    const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * 32;
+    const int ibase = img * p.h;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = threadIdx.x + u * 256;
+      const int q = i / NPX, px = i - q * NPX;
+      const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
+      const int co = co0 + 4 * q;
+      const bool ok = oh < p.h && ow < p.w && co < p.cout;
+      pdy[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co) * 4u : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = threadIdx.x + u * 256;
+      const int q = i / LPX, hp = i - q * LPX;
+      const int lr = hp / LW, lc = hp - lr * LW;
+      const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+      const int c = c0 + 4 * q;
+      const bool ok = i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
+      pxx[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c) * 4u : kOOB);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = threadIdx.x + u * 256;
+      const int q = i / NPX, px = i - q * NPX;
+      const int co = co0 + 4 * q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dyt[(4 * q + k) * DYS + px] = co + k < p.cout ? pdy[u][k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = threadIdx.x + u * 256;
+      if (i < xtotal) {
+        const int q = i / LPX, hp = i - q * LPX;
+        const int c = c0 + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xt[(4 * q + k) * LPX + hp] = c + k < p.cin ? pxx[u][k] : 0.f;
+      }
+    }
+  };
+  if (PF && tb < te) fetch(tb);
+  for (int tile = tb; tile < te; ++tile) {
+    __syncthreads();  // the previous tile's fragment reads are done
+    if (PF) {
+      store();
+    } else {  // lower register footprint: dY at once, X in batches of 4 loads per thread
+      const int img = tile / per_img;
+      const int trem = tile - img * per_img;
+      const int th = trem / p.tiles_w;
+      const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * 32;
+      const int ibase = img * p.h;
+      {
+        f4 v[NI];
+#pragma unroll
+        for (int u = 0; u < NI; ++u) {
+          const int i = threadIdx.x + u * 256;
+          const int q = i / NPX, px = i - q * NPX;
+          const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
+          const int co = co0 + 4 * q;
+          const bool ok = oh < p.h && ow < p.w && co < p.cout;
+          v[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co) * 4u : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < NI; ++u) {
+          const int i = threadIdx.x + u * 256;
+          const int q = i / NPX, px = i - q * NPX;
+          const int co = co0 + 4 * q;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            dyt[(4 * q + k) * DYS + px] = co + k < p.cout ? v[u][k] : 0.f;
+        }
+      }
+      for (int i0 = threadIdx.x; i0 < xtotal; i0 += 4 * 256) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256;
+          const int q = i / LPX, hp = i - q * LPX;
+          const int lr = hp / LW, lc = hp - lr * LW;
+          const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+          const int c = c0 + 4 * q;
+          const bool ok =
+              i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
+          v[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c) * 4u : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256;
+          if (i >= xtotal) break;
+          const int q = i / LPX, hp = i - q * LPX;
+          const int c = c0 + 4 * q;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) xt[(4 * q + k) * LPX + hp] = c + k < p.cin ? v[u][k] : 0.f;
+        }
+      }
+    }
+    __syncthreads();
+    if (PF && tile + 1 < te) fetch(tile + 1);
+#pragma unroll 2
+    for (int ch = 0; ch < NPX / 16; ++ch) {
+      const int px0 = ch * 16 + 4 * g;
+      const int poff = (px0 >> 5) * LW + (px0 & 31);
+      f4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const f4*>(&dyt[(i * 16 + r) * DYS + px0]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* b = &xt[bbase[j] + poff];
+        fb[j] = f4{b[0], b[1], b[2], b[3]};
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const int ncol4 = 9 * p.cin4;
+  float* out = p.part + (int64_t)blockIdx.x * p.cout * ncol4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = (wave * TN + j) * 16 + r;
+    const int t = n / p.csw;
+    const int cl = n - t * p.csw;
+    if (t >= 9 || cl >= csw_real) continue;
+    const int col = t * p.cin4 + c0 + cl;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + i * 16 + g * 4 + e;
+        if (co < p.cout) out[(int64_t)co * ncol4 + col] = acc[i][j][e];
+      }
+  }
+}
+
 // dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin4 + ci]
 // Block = 4 waves x 64 slab columns: lane = column (coalesced 256-B rows per split),
 // wave w sums splits w, w+4, ...; the 4 partial sums are combined in LDS in order.
@@ -834,6 +1038,88 @@ static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
   return ad->n * d.tiles_h * d.tiles_w;
 }
 
+// ---------------------------------------- direct 3x3 wgrad: host dispatch ----
+struct W3Tile {
+  int tm, tn, bh, csw, n_ci_slabs, n_co_slabs, tiles_h, tiles_w, ntiles, tps, splits;
+  bool pf;
+};
+
+static bool wgrad3_shape_ok(const vae2_act* xd, const vae2_act* dyd, int k, int stride, int pad) {
+  return k == 3 && stride == 1 && pad == 1 && xd->h == dyd->h && xd->w == dyd->w &&
+         xd->ps % 4 == 0 && dyd->ps % 4 == 0 && dyd->w >= 16;
+}
+
+static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd) {
+  W3Tile t;
+  const int cin4 = round_up((int)xd->c, 4);
+  int nsl = (cin4 + 35) / 36;  // up to 36 channels per slab
+  t.csw = round_up((int)ceil_div(cin4, nsl), 4);
+  t.n_ci_slabs = (int)ceil_div(cin4, t.csw);
+  const int nt = (9 * t.csw + 15) / 16;
+  t.tn = (nt + 3) / 4;
+  const int mt = (int)((dyd->c + 15) / 16);
+  t.n_co_slabs = (mt + 3) / 4;
+  t.tm = (mt + t.n_co_slabs - 1) / t.n_co_slabs;
+  t.bh = (t.tm <= 2 && t.csw <= 24) ? 8 : 4;
+  t.tiles_h = (int)ceil_div(dyd->h, t.bh);
+  t.tiles_w = (int)ceil_div(dyd->w, 32);
+  t.ntiles = (int)(dyd->n * t.tiles_h * t.tiles_w);
+  const int gy = t.n_ci_slabs * t.n_co_slabs;
+  // ~1024 workgroups in all and at most ~48 MB of partial slabs; layers with >= 1024
+  // tile-slabs use >= 2 tiles per workgroup and prefetch tile t+1 while t computes
+  int64_t want = ceil_div(1024, gy);
+  const int64_t slab = (int64_t)dyd->c * 9 * cin4 * 4;
+  const int64_t cap = 48ll << 20;
+  if (want * slab > cap) want = cap / slab > 0 ? cap / slab : 1;
+  if (want > t.ntiles) want = t.ntiles;
+  t.tps = (int)ceil_div(t.ntiles, want);
+  t.pf = (int64_t)t.ntiles * gy >= 1024;
+  if (t.pf) {
+    // one wave of workgroups: the prefetching variants hold 1 (TM >= 3) or 2
+    // workgroups per CU, so use exactly that many in all (no straggler wave)
+    const int64_t resident = t.tm >= 3 ? 256 : 512;
+    int64_t w2 = resident / gy > 0 ? resident / gy : 1;
+    if (w2 * slab > cap) w2 = cap / slab > 0 ? cap / slab : 1;
+    t.tps = (int)ceil_div(t.ntiles, w2);
+    if (t.tps < 2) t.tps = 2;
+  }
+  t.splits = (int)ceil_div(t.ntiles, t.tps);
+  return t;
+}
+
+static size_t wgrad3_lds(const W3Tile& t) {
+  const int npx = t.bh * 32, lpx = (t.bh + 2) * 34;
+  return ((size_t)16 * t.tm * (npx + 4) + (size_t)(t.csw + 1) * lpx) * sizeof(float);
+}
+
+template <int TM, int BH, bool PF>
+static void wgrad3_launch_tn(const WGrad3& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
+  switch (tn) {
+#define CASE(T) \
+  case T: hipLaunchKernelGGL((wgrad3_kernel<TM, T, BH, PF>), grid, dim3(256), shm, s, p); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
+#undef CASE
+  }
+}
+
+template <int BH, bool PF>
+static void wgrad3_launch_tm(const WGrad3& p, const W3Tile& t, dim3 grid, size_t shm,
+                             hipStream_t s) {
+  switch (t.tm) {
+    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, grid, shm, s); break;
+    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, grid, shm, s); break;
+    case 3: wgrad3_launch_tn<3, BH, PF>(p, t.tn, grid, shm, s); break;
+    default: wgrad3_launch_tn<4, BH, PF>(p, t.tn, grid, shm, s); break;
+  }
+}
+
+template <int BH>
+static void wgrad3_launch(const WGrad3& p, const W3Tile& t, dim3 grid, size_t shm,
+                          hipStream_t s) {
+  if (t.pf) wgrad3_launch_tm<BH, true>(p, t, grid, shm, s);
+  else wgrad3_launch_tm<BH, false>(p, t, grid, shm, s);
+}
+
 extern "C" {
 
 int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode) {
@@ -970,6 +1256,11 @@ int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, 
   int ncol4 = k * k * round_up((int)xd->c, 4);
   WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol4);
   int64_t part = (int64_t)t.splits * dyd->c * ncol4;
+  if (k == 3 && xd->h == dyd->h && xd->w == dyd->w) {  // the direct kernel may run instead
+    W3Tile t3 = pick_w3tile(xd, dyd);
+    const int64_t part3 = (int64_t)t3.splits * dyd->c * ncol4;
+    if (part3 > part) part = part3;
+  }
   int64_t bias_part = 2 * vae2_bn_partial_rows(dyd) * dyd->c;
   return part + bias_part + 4;
 }
@@ -986,7 +1277,30 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   hipStream_t s = as_stream(stream);
   const int cin4 = round_up((int)xd->c, 4);
   const int ncol4 = k * k * cin4;
+  int splits = 0;
+  if (g_conv_algo != 1 && wgrad3_shape_ok(xd, dyd, k, stride, pad) && vec_ok(x, (int)xd->ps) &&
+      vec_ok(dy, (int)dyd->ps)) {
+    W3Tile t3 = pick_w3tile(xd, dyd);
+    WGrad3 q{};
+    q.x = x; q.x_ps = (int)xd->ps; q.cin = (int)xd->c; q.cin4 = cin4;
+    q.h = (int)xd->h; q.w = (int)xd->w;
+    q.dy = dy; q.dy_ps = (int)dyd->ps; q.cout = (int)dyd->c;
+    q.tiles_h = t3.tiles_h; q.tiles_w = t3.tiles_w; q.ntiles = t3.ntiles;
+    q.tiles_per_split = t3.tps;
+    q.csw = t3.csw; q.n_ci_slabs = t3.n_ci_slabs;
+    q.x_bytes = act_bytes(xd); q.dy_bytes = act_bytes(dyd);
+    q.part = ws;
+    dim3 grid((unsigned)t3.splits, (unsigned)(t3.n_ci_slabs * t3.n_co_slabs));
+    const size_t shm = wgrad3_lds(t3);
+    if (t3.bh == 8) wgrad3_launch<8>(q, t3, grid, shm, s);
+    else wgrad3_launch<4>(q, t3, grid, shm, s);
+    int rc = check_launch(fn);
+    if (rc) return rc;
+    splits = t3.splits;
+  }
   WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol4);
+  if (splits) goto reduce;
+  {
   WGrad p{};
   p.x = x; p.x_ps = (int)xd->ps; p.cin = (int)xd->c; p.cin4 = cin4;
   p.x_h = (int)xd->h; p.x_w = (int)xd->w;
@@ -1010,14 +1324,20 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   }
   int rc = check_launch(fn);
   if (rc) return rc;
+  splits = t.splits;
+  }
+reduce:
   int64_t slab = dyd->c * (int64_t)ncol4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 64)), dim3(256), 0, s,
-                     (const float*)ws, t.splits, (int)dyd->c, (int)xd->c, cin4, k, dw,
+                     (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw,
                      accumulate);
-  rc = check_launch(fn);
+  int rc = check_launch(fn);
   if (rc) return rc;
   if (dbias) {
-    float* bp = ws + (int64_t)t.splits * dyd->c * ncol4;
+    // bias partial rows live after the largest partial-slab area the workspace holds
+    const int64_t part_max = vae2_conv2d_bwd_weight_ws_size(xd, dyd, k) - 4 -
+                             2 * vae2_bn_partial_rows(dyd) * dyd->c;
+    float* bp = ws + part_max;
     rc = vae2_bn_stats(dy, dyd, bp, stream);
     if (rc) return rc;
     rc = bias_grad_from_partials(bp, vae2_bn_partial_rows(dyd), dyd->c, dbias, accumulate,

@@ -54,6 +54,10 @@ def main():
                     help="vae2_conv2d_set_algo values to compare (0 auto, 1 gather, 2 direct)")
     a = ap.parse_args()
     lib = _lib.load()
+    warm = torch.randn(4096, 4096, device="cuda")
+    for _ in range(200):  # bring the clocks up before the first timed shape
+        warm = warm @ warm.T * 1e-4
+    torch.cuda.synchronize()
     for algo in a.algo:
         lib.vae2_conv2d_set_algo(algo)
         print(f"== algo {algo}")
