@@ -34,6 +34,8 @@ CONV_SHAPES = [
     (2, 8, 8, 154, 144, 3, 1, False),
     (2, 32, 64, 64, 64, 3, 1, False),
     (2, 8, 8, 270, 3, 1, 1, True),
+    (1, 128, 512, 72, 270, 1, 1, True),   # M = 65536: the wide-N 1x1 tiles (2 x 9)
+    (1, 64, 1024, 40, 130, 1, 1, False),  # wide, 9 tiles in one block
 ]
 
 
@@ -71,6 +73,10 @@ DIRECT_SHAPES = [
     (2, 5, 7, 3, 5, False),       # image smaller than one tile, TM = 2
     (1, 8, 32, 154, 144, False),  # 5 slabs (39 quads), N split over 3 blocks
     (2, 6, 33, 256, 18, True),    # 8 slabs, 2 column tiles of which one has 1 column
+    # 1x1 (the direct weight-gradient kernel's KS = 1 form; data paths: gather kernel)
+    (2, 8, 40, 270, 270, True, 1),
+    (1, 4, 64, 64, 256, False, 1),
+    (1, 5, 48, 18, 5, False, 1),
 ]
 
 
@@ -78,13 +84,14 @@ DIRECT_SHAPES = [
 def test_direct_conv3x3(shape):
     from vae2 import _lib, ops
     torch.manual_seed(3)
-    n, h, w, cin, cout, bias = shape
-    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias)
+    n, h, w, cin, cout, bias = shape[:6]
+    k = shape[6] if len(shape) > 6 else 3
+    conv = nn.Conv2d(cin, cout, k, 1, k // 2, bias=bias)
     x = torch.randn(n, cin, h, w, requires_grad=True)
     y_ref = conv(x)
     gy = torch.randn_like(y_ref)
     y_ref.backward(gy)
-    cg = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias).to(DEV)
+    cg = nn.Conv2d(cin, cout, k, 1, k // 2, bias=bias).to(DEV)
     cg.load_state_dict(conv.state_dict())
     lib = _lib.load()
     prev = lib.vae2_conv2d_set_algo(2)
@@ -99,8 +106,9 @@ def test_direct_conv3x3(shape):
         yg = ops.conv(xg, cg)
         yg.backward(dyg)
         torch.cuda.synchronize()
-        name = ctypes_name(xg, (n, h, w, cout))
-        assert name.startswith("dconv3_kernel"), name
+        if k == 3:
+            name = ctypes_name(xg, (n, h, w, cout))
+            assert name.startswith("dconv3_kernel"), name
     finally:
         lib.vae2_conv2d_set_algo(prev)
     assert rel(nchw(yg), y_ref) < TOL

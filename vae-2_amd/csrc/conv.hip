@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  auto load = [&](f4* fa, f4* fb) {
+  auto load = [&](f4* fa, f4* fb, int& mk) {
     const bool tv = tt < ntaps;
     const int tc = tv ? tt : 0;
     const int th = tc / p.ntw;
@@ -195,12 +195,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
       const uint32_t off = ok ? (uint32_t)((rpix[i] + doff) * p.a_ps + c0) * 4u : kOOB;
       f4 v;
       if (VEC) {
-        v = load4(arsrc, off);
-        if (cpad) {
-          v[1] = m1 ? v[1] : 0.f;
-          v[2] = m2 ? v[2] : 0.f;
-          v[3] = m3 ? v[3] : 0.f;
-        }
+        v = load4(arsrc, off);  // channel-pad lanes are masked where consumed (mma)
       } else {
         v[0] = load1(arsrc, off);
         v[1] = load1(arsrc, m1 ? off + 4u : kOOB);
@@ -209,10 +204,21 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
       }
       fa[i] = v;
     }
+    mk = (m1 ? 2 : 0) | (m2 ? 4 : 0) | (m3 ? 8 : 0);
     c0 += 16;
     while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
   };
-  auto mma = [&](const f4* fa, const f4* fb) {
+  // Masking the pad lanes here (not right after the loads) keeps the next chunk's
+  // loads in flight across this chunk's MFMAs.
+  auto mma = [&](f4* fa, const f4* fb, int mk) {
+    if (VEC && cpad) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        fa[i][1] = (mk & 2) ? fa[i][1] : 0.f;
+        fa[i][2] = (mk & 4) ? fa[i][2] : 0.f;
+        fa[i][3] = (mk & 8) ? fa[i][3] : 0.f;
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -224,12 +230,13 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
 
   // Chunk pairs; the (possibly) extra odd chunk loads zeros (tt >= ntaps).
   if (mw < M) {
-    load(fa0, fb0);
+    int mk0 = 0, mk1 = 0;
+    load(fa0, fb0, mk0);
     for (int ch = 0; ch < nchunks; ch += 2) {
-      load(fa1, fb1);
-      mma(fa0, fb0);
-      load(fa0, fb0);
-      mma(fa1, fb1);
+      load(fa1, fb1, mk1);
+      mma(fa0, fb0, mk0);
+      load(fa0, fb0, mk0);
+      mma(fa1, fb1, mk1);
     }
   }
 
@@ -473,9 +480,23 @@ struct Tile {
   int tm, tn, nblk;
 };
 
-static Tile pick_tile(int64_t M, int N) {
+static int g_wide_tiles = 1;
+
+// 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
+// 32 rows, so the activation rows are re-read by 2 column blocks instead of 5.
+static bool wide_ok(int64_t M, int N, int taps) {
+  return g_wide_tiles && taps == 1 && N > 64 && M >= 65536;
+}
+
+static Tile pick_tile(int64_t M, int N, bool wide = false) {
   Tile t;
   int tiles = (N + 15) / 16;
+  if (wide && tiles > 4) {
+    t.nblk = (tiles + 8) / 9;
+    t.tn = (tiles + t.nblk - 1) / t.nblk;
+    t.tm = 2;
+    return t;
+  }
   if (tiles <= 4) {
     t.tn = tiles;
     t.nblk = 1;
@@ -499,8 +520,19 @@ static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
 }
 
 template <bool VEC, int ROLE>
+static void launch_wide(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
+  switch (tn) {
+#define CASE(T) \
+  case T: hipLaunchKernelGGL((igemm_kernel<2, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
+    CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
+#undef CASE
+  }
+}
+
+template <bool VEC, int ROLE>
 static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
-  if (t.tm == 4) launch_tn<4, VEC, ROLE>(p, t.tn, grid, s);
+  if (t.tm == 2 && t.tn > 4) launch_wide<VEC, ROLE>(p, t.tn, grid, s);
+  else if (t.tm == 4) launch_tn<4, VEC, ROLE>(p, t.tn, grid, s);
   else if (t.tm == 2) launch_tn<2, VEC, ROLE>(p, t.tn, grid, s);
   else launch_tn<1, VEC, ROLE>(p, t.tn, grid, s);
 }
@@ -512,7 +544,7 @@ static bool vec_ok(const float* a, int ps) {
 static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn) {
   int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
   if (M == 0) return 0;
-  Tile t = pick_tile(M, p.n);
+  Tile t = pick_tile(M, p.n, wide_ok(M, p.n, p.nth * p.ntw));
   p.hw_div = FastDiv((uint32_t)(p.g_h * p.g_w));
   p.w_div = FastDiv((uint32_t)p.g_w);
   dim3 grid((unsigned)ceil_div(M, 64 * t.tm), (unsigned)t.nblk);
@@ -527,8 +559,8 @@ static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn) {
   return check_launch(fn);
 }
 
-static int64_t igemm_rows(int64_t M, int N) {
-  Tile t = pick_tile(M, N);
+static int64_t igemm_rows(int64_t M, int N, int taps) {
+  Tile t = pick_tile(M, N, wide_ok(M, N, taps));
   return ceil_div(M, 64 * t.tm);
 }
 
@@ -678,9 +710,11 @@ struct WGrad3 {
   float* part;  // [splits][cout][9*cin4]
 };
 
-template <int TM, int TN, int BH, bool PF>
+template <int TM, int TN, int BH, bool PF, int KS>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
-  constexpr int LH = BH + 2, LW = 34, NPX = BH * 32, LPX = LH * LW;
+  constexpr int HALO = KS / 2, TAPS = KS * KS;
+  constexpr int LH = BH + KS - 1, LW = 32 + KS - 1, NPX = BH * 32, LPX = LH * LW;
+  constexpr int QMAX = KS == 1 ? 16 : 9;  // channel quads per slab
   constexpr int DYS = NPX + 4;  // dY^T row stride (floats)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dyt = sm;                  // [16*TM][DYS]
@@ -699,8 +733,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     const int n = (wave * TN + j) * 16 + r;
     const int t = n / p.csw;
     const int cl = n - t * p.csw;
-    const bool ok = t < 9 && cl < csw_real;
-    bbase[j] = ok ? cl * LPX + (t / 3) * LW + (t % 3) : p.csw * LPX;
+    const bool ok = t < TAPS && cl < csw_real;
+    bbase[j] = ok ? cl * LPX + (t / KS) * LW + (t % KS) : p.csw * LPX;
   }
   for (int i = threadIdx.x; i < LPX; i += 256) xt[p.csw * LPX + i] = 0.f;
 
@@ -715,7 +749,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   const int te = tb + p.tiles_per_split < p.ntiles ? tb + p.tiles_per_split : p.ntiles;
   // Register prefetch: tile t+1's global loads are in flight while tile t computes.
   constexpr int NI = NPX * 4 * TM / 256;     // dY items per thread
-  constexpr int NX = (LPX * 9 + 255) / 256;  // X items per thread (<= 9 quads per slab)
+  constexpr int NX = (LPX * QMAX + 255) / 256;  // X items per thread
   const int xtotal = LPX * (csw_real >> 2);
   f4 pdy[NI], pxx[NX];
   auto fetch = [&](int tile) {
@@ -738,7 +772,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
       const int i = threadIdx.x + u * 256;
       const int q = i / LPX, hp = i - q * LPX;
       const int lr = hp / LW, lc = hp - lr * LW;
-      const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+      const int ih = oh0 - HALO + lr, iw = ow0 - HALO + lc;
       const int c = c0 + 4 * q;
       const bool ok = i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
       pxx[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c) * 4u : kOOB);
@@ -803,7 +837,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
           const int i = i0 + u * 256;
           const int q = i / LPX, hp = i - q * LPX;
           const int lr = hp / LW, lc = hp - lr * LW;
-          const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+          const int ih = oh0 - HALO + lr, iw = ow0 - HALO + lc;
           const int c = c0 + 4 * q;
           const bool ok =
               i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
@@ -833,7 +867,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const float* b = &xt[bbase[j] + poff];
-        fb[j] = f4{b[0], b[1], b[2], b[3]};
+        if (KS == 1) fb[j] = *reinterpret_cast<const f4*>(b);  // 16-byte aligned: no tap shift
+        else fb[j] = f4{b[0], b[1], b[2], b[3]};
       }
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
@@ -845,14 +880,14 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     }
   }
 
-  const int ncol4 = 9 * p.cin4;
+  const int ncol4 = TAPS * p.cin4;
   float* out = p.part + (int64_t)blockIdx.x * p.cout * ncol4;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = (wave * TN + j) * 16 + r;
     const int t = n / p.csw;
     const int cl = n - t * p.csw;
-    if (t >= 9 || cl >= csw_real) continue;
+    if (t >= TAPS || cl >= csw_real) continue;
     const int col = t * p.cin4 + c0 + cl;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1040,27 +1075,31 @@ static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
 
 // ---------------------------------------- direct 3x3 wgrad: host dispatch ----
 struct W3Tile {
-  int tm, tn, bh, csw, n_ci_slabs, n_co_slabs, tiles_h, tiles_w, ntiles, tps, splits;
+  int ks, tm, tn, bh, csw, n_ci_slabs, n_co_slabs, tiles_h, tiles_w, ntiles, tps, splits;
   bool pf;
 };
 
 static bool wgrad3_shape_ok(const vae2_act* xd, const vae2_act* dyd, int k, int stride, int pad) {
-  return k == 3 && stride == 1 && pad == 1 && xd->h == dyd->h && xd->w == dyd->w &&
-         xd->ps % 4 == 0 && dyd->ps % 4 == 0 && dyd->w >= 16;
+  // (the KS = 1 form of the kernel measured slower than the gather kernel on 1x1 convs:
+  //  without the 9-tap reuse the staging does not pay for itself)
+  return k == 3 && pad == 1 && stride == 1 && xd->h == dyd->h &&
+         xd->w == dyd->w && xd->ps % 4 == 0 && dyd->ps % 4 == 0 && dyd->w >= 16;
 }
 
-static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd) {
+static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
   W3Tile t;
+  t.ks = k;
   const int cin4 = round_up((int)xd->c, 4);
-  int nsl = (cin4 + 35) / 36;  // up to 36 channels per slab
+  const int maxc = k == 1 ? 64 : 36;  // channels per slab (columns = taps x channels)
+  int nsl = (cin4 + maxc - 1) / maxc;
   t.csw = round_up((int)ceil_div(cin4, nsl), 4);
   t.n_ci_slabs = (int)ceil_div(cin4, t.csw);
-  const int nt = (9 * t.csw + 15) / 16;
+  const int nt = (k * k * t.csw + 15) / 16;
   t.tn = (nt + 3) / 4;
   const int mt = (int)((dyd->c + 15) / 16);
   t.n_co_slabs = (mt + 3) / 4;
   t.tm = (mt + t.n_co_slabs - 1) / t.n_co_slabs;
-  t.bh = (t.tm <= 2 && t.csw <= 24) ? 8 : 4;
+  t.bh = (t.tm <= 2 && t.csw <= 24 && k == 3) ? 8 : 4;
   t.tiles_h = (int)ceil_div(dyd->h, t.bh);
   t.tiles_w = (int)ceil_div(dyd->w, 32);
   t.ntiles = (int)(dyd->n * t.tiles_h * t.tiles_w);
@@ -1068,7 +1107,7 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd) {
   // ~1024 workgroups in all and at most ~48 MB of partial slabs; layers with >= 1024
   // tile-slabs use >= 2 tiles per workgroup and prefetch tile t+1 while t computes
   int64_t want = ceil_div(1024, gy);
-  const int64_t slab = (int64_t)dyd->c * 9 * cin4 * 4;
+  const int64_t slab = (int64_t)dyd->c * k * k * cin4 * 4;
   const int64_t cap = 48ll << 20;
   if (want * slab > cap) want = cap / slab > 0 ? cap / slab : 1;
   if (want > t.ntiles) want = t.ntiles;
@@ -1088,15 +1127,20 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd) {
 }
 
 static size_t wgrad3_lds(const W3Tile& t) {
-  const int npx = t.bh * 32, lpx = (t.bh + 2) * 34;
+  const int npx = t.bh * 32, lpx = (t.bh + t.ks - 1) * (32 + t.ks - 1);
   return ((size_t)16 * t.tm * (npx + 4) + (size_t)(t.csw + 1) * lpx) * sizeof(float);
 }
 
 template <int TM, int BH, bool PF>
-static void wgrad3_launch_tn(const WGrad3& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
+static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
+                             hipStream_t s) {
+  if (ks == 1) {  // 1x1: at most 64 channels = 4 column tiles per slab, one per wave
+    hipLaunchKernelGGL((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
+    return;
+  }
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((wgrad3_kernel<TM, T, BH, PF>), grid, dim3(256), shm, s, p); break;
+  case T: hipLaunchKernelGGL((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
 #undef CASE
   }
@@ -1106,10 +1150,10 @@ template <int BH, bool PF>
 static void wgrad3_launch_tm(const WGrad3& p, const W3Tile& t, dim3 grid, size_t shm,
                              hipStream_t s) {
   switch (t.tm) {
-    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, grid, shm, s); break;
-    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, grid, shm, s); break;
-    case 3: wgrad3_launch_tn<3, BH, PF>(p, t.tn, grid, shm, s); break;
-    default: wgrad3_launch_tn<4, BH, PF>(p, t.tn, grid, shm, s); break;
+    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
+    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
+    case 3: wgrad3_launch_tn<3, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
+    default: wgrad3_launch_tn<4, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
   }
 }
 
@@ -1148,8 +1192,11 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
 }
 
 int vae2_conv2d_set_algo(int algo) {
-  const int prev = g_conv_algo;
-  if (algo >= 0 && algo <= 2) g_conv_algo = algo;
+  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4);
+  if (algo >= 0 && algo <= 6 && algo != 3) {
+    g_conv_algo = algo & 3;
+    g_wide_tiles = algo < 4;
+  }
   return prev;
 }
 
@@ -1157,7 +1204,7 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
                                    int k, int stride, int pad) {
   if (!act_ok(xd) || !act_ok(yd)) return 0;
   if (dconv_use(xd, yd, k, stride, pad, x)) return dconv_rows(xd, yd);
-  return igemm_rows(act_pixels(yd), (int)yd->c);
+  return igemm_rows(act_pixels(yd), (int)yd->c, k * k);
 }
 
 int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, int stride,
@@ -1168,7 +1215,7 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
     snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
     return 0;
   }
-  Tile t = pick_tile(act_pixels(yd), (int)yd->c);
+  Tile t = pick_tile(act_pixels(yd), (int)yd->c, wide_ok(act_pixels(yd), (int)yd->c, k * k));
   snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0>", t.tm, t.tn);
   return 0;
 }
@@ -1256,8 +1303,8 @@ int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, 
   int ncol4 = k * k * round_up((int)xd->c, 4);
   WTile t = pick_wtile(act_pixels(dyd), (int)dyd->c, ncol4);
   int64_t part = (int64_t)t.splits * dyd->c * ncol4;
-  if (k == 3 && xd->h == dyd->h && xd->w == dyd->w) {  // the direct kernel may run instead
-    W3Tile t3 = pick_w3tile(xd, dyd);
+  if ((k == 3 || k == 1) && xd->h == dyd->h && xd->w == dyd->w) {  // direct kernel may run
+    W3Tile t3 = pick_w3tile(xd, dyd, k);
     const int64_t part3 = (int64_t)t3.splits * dyd->c * ncol4;
     if (part3 > part) part = part3;
   }
@@ -1280,7 +1327,7 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   int splits = 0;
   if (g_conv_algo != 1 && wgrad3_shape_ok(xd, dyd, k, stride, pad) && vec_ok(x, (int)xd->ps) &&
       vec_ok(dy, (int)dyd->ps)) {
-    W3Tile t3 = pick_w3tile(xd, dyd);
+    W3Tile t3 = pick_w3tile(xd, dyd, k);
     WGrad3 q{};
     q.x = x; q.x_ps = (int)xd->ps; q.cin = (int)xd->c; q.cin4 = cin4;
     q.h = (int)xd->h; q.w = (int)xd->w;
