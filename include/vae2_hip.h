@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 2
+#define VAE2_ABI_VERSION 3
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -60,14 +60,21 @@ int vae2_conv2d_set_algo(int algo);
 int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode);
 int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k,
                             int mode, float* out, void* stream);
+/* The same from a block of input channels of a wider weight: element (co, ci, t)
+ * is read at w[co*ld + ci*k*k + t] (ld >= cin*k*k; pass w + c0*k*k for the block
+ * starting at input channel c0).                                                */
+int vae2_conv2d_pack_weight_ld(const float* w, int64_t cout, int64_t cin, int k,
+                               int mode, int64_t ld, float* out, void* stream);
 
 /* Many packings in one launch (a model's whole weight set after each optimizer
  * step).  `jobs` is a DEVICE array of njobs descriptors; `out` buffers must not
  * overlap.  Replaces the per-conv weight reads of F.conv2d (enc_hrnet.py:27-30). */
 typedef struct vae2_pack_job {
-  const float* w;  /* [cout][cin][k][k] */
+  const float* w;  /* [cout][cin][k][k], rows ld floats apart */
   float* out;      /* vae2_conv2d_packed_size(cout, cin, k, mode) floats */
   int32_t cout, cin, k, mode;
+  int32_t ld;      /* 0: cin*k*k (a whole weight), else as vae2_conv2d_pack_weight_ld */
+  int32_t pad_;
 } vae2_pack_job;
 int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* stream);
 
@@ -103,6 +110,13 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
                            const vae2_act* dyd, float* dw, float* dbias, int k,
                            int stride, int pad, int accumulate, float* ws,
                            int64_t ws_size, void* stream);
+
+/* vae2_conv2d_bwd_weight writing dW rows dw_ld floats apart (an input-channel
+ * block of a wider weight's gradient: dw = grad + c0*k*k, dw_ld = Cin_total*k*k). */
+int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* dy,
+                              const vae2_act* dyd, float* dw, int64_t dw_ld, float* dbias,
+                              int k, int stride, int pad, int accumulate, float* ws,
+                              int64_t ws_size, void* stream);
 
 /* ------------------------------------------------------------ batchnorm ---- */
 /* nn.BatchNorm2d(momentum=0.01, eps=1e-5) in train mode, enc_hrnet.py:22-23,
@@ -177,6 +191,51 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
                            int relu, float* dx, const vae2_act* dxd,
                            float* dres, const vae2_act* dresd, void* stream);
 
+/* ---------------------------------------------------------- head output ---- */
+/* 1x1 conv of a channel-concatenation of bilinearly upsampled maps, computed per
+ * block of input channels (the HRNet heads, enc_hrnet.py:833-847, :889-905, :947-963:
+ * Conv1x1(cat[x0, up(x1), up(x2), up(x3)])).  A 1x1 conv commutes with the
+ * upsampling, so with W = [W0 | W1 | W2 | W3] split by input block
+ *     y = W0 x0 + bias + up(W1 x1) + up(W2 x2) + up(W3 x3),
+ * the z_s = W_s x_s computed at their own resolution (vae2_conv2d_fwd).  This call:
+ * y = conv1x1(x, w) + bias + sum_s bilinear_up(ups[s]) to y's h, w (align_corners=False;
+ * channels [0, yd->c) of each ups[s], nup <= 3), w = the [Cout][Cin0] block of a 1x1
+ * weight with rows w_ld floats apart (Cin0 <= 32); optional BN partial statistics
+ * stats [2][vae2_conv1x1_upsum_stats_rows(yd)][Cout].                              */
+int64_t vae2_conv1x1_upsum_stats_rows(const vae2_act* yd);
+int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, int64_t w_ld,
+                           const float* bias, int nup, const float* const* ups,
+                           const vae2_act* upds, float* y, const vae2_act* yd, float* stats,
+                           void* stream);
+
+/* The HRNet head after its wide 1x1 conv (enc_hrnet.py:323-370, applied at
+ * :839-847, :897-905, :955-963): BatchNorm (coefficients `save` [4][C] from
+ * vae2_bn_reduce_finalize / _finalize) -> ReLU -> Conv1x1(C -> cout2 <= 4, bias),
+ * reading the pre-BN conv output y once per pass; the ReLU output is never stored.
+ * y: 16-byte aligned NHWC, ps % 4 == 0, C <= 1024.  w2 = [cout2][C] (the conv weight
+ * [cout2][C][1][1]), b2 = [cout2] or NULL.
+ *   out[p][o] = b2[o] + sum_c w2[o][c] * relu(y[p][c]*scale[c] + shift[c])        */
+int vae2_head_out_fwd(const float* y, const vae2_act* yd, const float* save, const float* w2,
+                      const float* b2, int cout2, float* out, const vae2_act* outd,
+                      void* stream);
+/* Workspace (floats) of the two backward calls.                                   */
+int64_t vae2_head_out_bwd_ws_size(const vae2_act* yd, int cout2);
+/* Backward, part 1 (local sums; SyncBN all-reduces `sums` before part 2):
+ * g = (w2^T dout) * [relu input > 0];  sums[2][C] = (sum g, sum g*xhat) in double;
+ * dgamma += sum g*xhat, dbeta += sum g, dw2 += sum dout (x) relu_out, db2 += sum dout
+ * (any of the four may be NULL).                                                   */
+int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* save,
+                             const float* w2, int cout2, const float* dout,
+                             const vae2_act* doutd, double* sums, float* dgamma, float* dbeta,
+                             float* dw2, float* db2, float* ws, int64_t ws_size, void* stream);
+/* Backward, part 2: dy = gamma*invstd*(g - sums[0]/count - xhat*sums[1]/count) (the
+ * gradient w.r.t. the wide conv's output), dbias += sum_p dy when dbias != NULL.     */
+int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* save,
+                            const float* gamma, const float* w2, int cout2, const float* dout,
+                            const vae2_act* doutd, const double* sums, double count, float* dy,
+                            const vae2_act* dyd, float* dbias, float* ws, int64_t ws_size,
+                            void* stream);
+
 /* ----------------------------------------------- resample / fuse / concat ---- */
 
 /* y (+)= bilinear_upsample(x) to y's h,w, align_corners=False
@@ -192,6 +251,15 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
  * are bilinearly upsampled (HighResolutionModule fuse, enc_hrnet.py:233-249). */
 int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
                        float* y, const vae2_act* yd, void* stream);
+
+/* dxs[s] = adjoint of bilinear_up (align_corners=False) applied to dy, for n <= 3
+ * lower-resolution targets at once, reading dy once (separable: a horizontal pass into
+ * the workspace, then a vertical pass per target).  dxs[s] have dy's channel count.  */
+int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
+                                                 const vae2_act* dxds);
+int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n,
+                                     float* const* dxs, const vae2_act* dxds, float* ws,
+                                     int64_t ws_size, void* stream);
 
 /* g = dy * (y > 0)  (ReLU backward, threshold_backward).                       */
 int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,

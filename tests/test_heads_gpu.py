@@ -1,0 +1,127 @@
+"""Per-branch head path (vae2/heads.py) against the reference's formulation in fp64.
+
+Reference (enc_hrnet.py:833-847, :323-370): x = cat([y0, up(y1), up(y2), up(y3)]),
+out_k = Conv1x1(ReLU(BN_train(Conv1x1(x)))), cat over k.  The HIP path computes the
+wide conv per branch at the branch resolution; it is the same linear map, so it is
+held to fp64 of the reference formulation at fp32 accuracy: outputs and running
+statistics 1e-5 relative; every input / parameter gradient within relative-L2
+max(1e-4, 3 x the distance of the reference formulation run in fp32) of fp64 (the BN
+backward cancels, so fp32 gradient accuracy falls with the pixel count for any
+implementation; the conv biases in front of BN have an analytically zero gradient and
+are held to an absolute bound against the gradient scale instead).
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import build, make_cfg, max_rel, rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def ref_heads(heads, ys):
+    """fp64 reference formulation on NCHW tensors (the reference's own op sequence)."""
+    H, W = ys[0].shape[2:]
+    x = torch.cat([ys[0]] + [F.interpolate(y, size=(H, W), mode="bilinear", align_corners=False)
+                             for y in ys[1:]], 1)
+    outs = []
+    for h in heads:
+        r = F.conv2d(x, h[0].weight, h[0].bias)
+        r = F.batch_norm(r, h[1].running_mean, h[1].running_var, h[1].weight, h[1].bias,
+                         training=True, momentum=h[1].momentum, eps=h[1].eps)
+        outs.append(F.conv2d(F.relu(r), h[3].weight, h[3].bias))
+    return torch.cat(outs, 1)
+
+
+def _heads_and_inputs(arch, hw, n, seed=0):
+    ed, _ = build(make_cfg(arch, hw=hw))
+    heads = [getattr(ed, f"last_layer_{k}") for k in (1, 2, 3)]
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for h in heads:  # O(1) activations (the reference init std 0.001 makes BN see ~0)
+            for m in (h[0], h[3]):
+                m.weight.normal_(0, (1.0 / m.in_channels) ** 0.5, generator=g)
+                m.bias.normal_(0, 0.1, generator=g)
+            h[1].weight.uniform_(0.5, 1.5, generator=g)
+            h[1].bias.normal_(0, 0.1, generator=g)
+    split = ed.last_stage_channels
+    sizes = [hw]
+    for _ in split[1:]:
+        h_, w_ = sizes[-1]
+        sizes.append(((h_ + 1) // 2, (w_ + 1) // 2))  # stride-2 3x3 convs
+    ys = [torch.randn(n, c, s[0], s[1], generator=g) for c, s in zip(split, sizes)]
+    return heads, ys
+
+
+@pytest.mark.parametrize("arch,hw,n", [("w18", (32, 64), 2), ("tiny", (30, 22), 3),
+                                       ("w18", (34, 50), 2), ("w18", (64, 128), 2)])
+def test_heads_match_reference_formulation(arch, hw, n):
+    from vae2 import heads as vheads
+    heads, ys = _heads_and_inputs(arch, hw, n)
+    assert vheads.supported(heads, [y.shape[1] for y in ys])
+    ref_h = [copy.deepcopy(h).double() for h in heads]
+    ys_ref = [y.double().requires_grad_() for y in ys]
+    out_ref = ref_heads(ref_h, ys_ref)
+    gout = torch.randn(out_ref.shape, generator=torch.Generator().manual_seed(7),
+                       dtype=torch.float64)
+    (out_ref * gout).sum().backward()
+    f32_h = [copy.deepcopy(h).float() for h in heads]
+    ys_f32 = [y.clone().requires_grad_() for y in ys]
+    (ref_heads(f32_h, ys_f32) * gout.float()).sum().backward()
+
+    def tol(a32, a64):
+        return max(1e-4, 3 * rel(a32, a64))
+
+    hip_h = [copy.deepcopy(h).to(DEV) for h in heads]
+    ys_hip = [y.detach().permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_() for y in ys]
+    out = vheads.run(hip_h, ys_hip)
+    out.backward(gout.float().permute(0, 2, 3, 1).contiguous().to(DEV))
+    torch.cuda.synchronize()
+
+    got = out.detach().permute(0, 3, 1, 2).cpu()
+    assert max_rel(got, out_ref) < 1e-5, max_rel(got, out_ref)
+    for yh, yr, y32 in zip(ys_hip, ys_ref, ys_f32):
+        e = rel(yh.grad.permute(0, 3, 1, 2), yr.grad)
+        assert e < tol(y32.grad, yr.grad), (e, rel(y32.grad, yr.grad))
+    for hh, hr, h32 in zip(hip_h, ref_h, f32_h):
+        for (name, p), (_, pr), (_, p32) in zip(hh.named_parameters(), hr.named_parameters(),
+                                                h32.named_parameters()):
+            if name == "0.bias":  # analytically zero in front of BN: rounding-level only
+                scale = float(hr[0].weight.grad.abs().max())
+                assert float(p.grad.abs().max()) < 1e-4 * scale, (name, p.grad.abs().max())
+                continue
+            e = rel(p.grad, pr.grad)
+            assert e < tol(p32.grad, pr.grad), (name, e, rel(p32.grad, pr.grad))
+        for name in ("running_mean", "running_var"):
+            a, b = getattr(hh[1], name), getattr(hr[1], name)
+            assert max_rel(a, b) < 1e-5, (name, max_rel(a, b))
+        assert int(hh[1].num_batches_tracked) == 1  # (F.batch_norm does not count)
+
+
+def test_heads_packed_cols_follow_optimizer_updates():
+    """The PackPlan's per-branch packed blocks track in-place weight updates."""
+    from vae2 import heads as vheads
+    from vae2.optim import FusedAdam
+    heads, ys = _heads_and_inputs("tiny", (16, 16), 2)
+    mod = torch.nn.ModuleList(heads).to(DEV)
+    opt = FusedAdam([mod], lr=1e-2)
+    ys_d = [y.permute(0, 2, 3, 1).contiguous().to(DEV) for y in ys]
+    for _ in range(2):
+        opt.zero_grad()
+        out = vheads.run(list(mod), ys_d)
+        out.square().sum().backward()
+        opt.step()
+    # after the updates, a fresh eager evaluation must equal the reference formulation
+    ref_h = [copy.deepcopy(h).double().cpu() for h in mod]
+    for h in ref_h:  # undo the running-stat updates of the HIP forward we compare against
+        h[1].reset_running_stats()
+    with torch.no_grad():
+        hip_h = [copy.deepcopy(h) for h in mod]
+        for h in hip_h:
+            h[1].reset_running_stats()
+        got = vheads.run(hip_h, ys_d).permute(0, 3, 1, 2).cpu()
+        want = ref_heads(ref_h, [y.double() for y in ys])
+    assert max_rel(got, want) < 1e-5, max_rel(got, want)

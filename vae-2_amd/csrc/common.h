@@ -68,6 +68,36 @@ struct FastDiv {
   }
 };
 
+// ------------------------------------------------- bilinear helpers ----
+// PyTorch's area_pixel_compute_source_index for align_corners=False, in fp32.
+struct Lerp {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lerp lerp_index(int dst, int in_size, float scale) {
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  int i0 = (int)src;
+  if (i0 > in_size - 1) i0 = in_size - 1;
+  int ip = (i0 < in_size - 1) ? 1 : 0;
+  Lerp l;
+  l.i0 = i0;
+  l.i1 = i0 + ip;
+  l.l1 = src - (float)i0;
+  l.l0 = 1.f - l.l1;
+  return l;
+}
+
+// Weight with which output coordinate `o` reads input coordinate `i`.
+__device__ __forceinline__ float lerp_weight(int o, int in_size, float scale, int i) {
+  Lerp l = lerp_index(o, in_size, scale);
+  float w = 0.f;
+  if (l.i0 == i) w += l.l0;
+  if (l.i1 == i) w += l.l1;
+  return w;
+}
+
 // Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream);

@@ -61,9 +61,11 @@ __device__ __forceinline__ float load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // ------------------------------------------------------------ weight pack ----
 // mode 0: out[n][t][c4] = w[n][c][t]         n < round_up(cout,64), c4 < round_up(cin,4)
 // mode 1: out[n][t][c4] = w[c][n][t]         n < round_up(cin,64),  c4 < round_up(cout,4)
-// (rows padded to 64 = the widest N tile, so B loads never need a bounds check)
+// (rows padded to 64 = the widest N tile, so B loads never need a bounds check).
+// w[co][ci][t] lives at w[co*ld + ci*kk + t]: ld = cin*kk for a whole weight, larger
+// for an input-channel block of a wider one (the per-branch blocks of a head conv).
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int kk,
-                                   int mode, float* __restrict__ out) {
+                                   int mode, int ld, float* __restrict__ out) {
   const int rows = mode == 0 ? (cout + 63) / 64 * 64 : (cin + 63) / 64 * 64;
   const int cols4 = mode == 0 ? (cin + 3) / 4 * 4 : (cout + 3) / 4 * 4;
   const int total = rows * kk * cols4;
@@ -74,9 +76,9 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int ci
     int c = rem - t * cols4;
     float v = 0.f;
     if (mode == 0) {
-      if (n < cout && c < cin) v = w[((int64_t)n * cin + c) * kk + t];
+      if (n < cout && c < cin) v = w[(int64_t)n * ld + c * kk + t];
     } else {
-      if (n < cin && c < cout) v = w[((int64_t)c * cin + n) * kk + t];
+      if (n < cin && c < cout) v = w[(int64_t)c * ld + n * kk + t];
     }
     out[i] = v;
   }
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pa
   const int cols4 = j.mode == 0 ? (j.cin + 3) / 4 * 4 : (j.cout + 3) / 4 * 4;
   const int per_row = kk * cols4;
   const int total = rows * per_row;
+  const int64_t ld = j.ld > 0 ? j.ld : (int64_t)j.cin * kk;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int n = i / per_row;
     const int rem = i - n * per_row;
@@ -97,9 +100,9 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pa
     const int c = rem - t * cols4;
     float v = 0.f;
     if (j.mode == 0) {
-      if (n < j.cout && c < j.cin) v = j.w[((int64_t)n * j.cin + c) * kk + t];
+      if (n < j.cout && c < j.cin) v = j.w[(int64_t)n * ld + c * kk + t];
     } else {
-      if (n < j.cin && c < j.cout) v = j.w[((int64_t)c * j.cin + n) * kk + t];
+      if (n < j.cin && c < j.cout) v = j.w[(int64_t)c * ld + n * kk + t];
     }
     j.out[i] = v;
   }
@@ -905,7 +908,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                            int splits, int cout, int cin,
                                                            int cin4, int k,
-                                                           float* __restrict__ dw,
+                                                           float* __restrict__ dw, int64_t ld,
                                                            int accumulate) {
   __shared__ float red[4][64];
   const int kk = k * k;
@@ -929,7 +932,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const int t = col / cin4;
   const int ci = col - t * cin4;
   if (ci >= cin) return;
-  const int64_t o = ((int64_t)co * cin + ci) * kk + t;
+  const int64_t o = (int64_t)co * ld + ci * kk + t;
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
@@ -1172,15 +1175,21 @@ int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode) {
   return (int64_t)rows * k * k * cols4;
 }
 
-int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k, int mode,
-                            float* out, void* stream) {
+int vae2_conv2d_pack_weight_ld(const float* w, int64_t cout, int64_t cin, int k, int mode,
+                               int64_t ld, float* out, void* stream) {
   const char* fn = "vae2_conv2d_pack_weight";
   VAE2_REQUIRE(w && out && cout > 0 && cin > 0 && k > 0 && (mode == 0 || mode == 1), fn,
                "bad arguments");
+  VAE2_REQUIRE(ld >= cin * k * k && ld < (int64_t(1) << 31), fn, "bad row stride");
   int64_t total = vae2_conv2d_packed_size(cout, cin, k, mode);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0,
-                     as_stream(stream), w, (int)cout, (int)cin, k * k, mode, out);
+                     as_stream(stream), w, (int)cout, (int)cin, k * k, mode, (int)ld, out);
   return check_launch(fn);
+}
+
+int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k, int mode,
+                            float* out, void* stream) {
+  return vae2_conv2d_pack_weight_ld(w, cout, cin, k, mode, cin * k * k, out, stream);
 }
 
 int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* stream) {
@@ -1312,11 +1321,12 @@ int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, 
   return part + bias_part + 4;
 }
 
-int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
-                           const vae2_act* dyd, float* dw, float* dbias, int k,
-                           int stride, int pad, int accumulate, float* ws,
-                           int64_t ws_size, void* stream) {
+int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* dy,
+                              const vae2_act* dyd, float* dw, int64_t dw_ld, float* dbias,
+                              int k, int stride, int pad, int accumulate, float* ws,
+                              int64_t ws_size, void* stream) {
   const char* fn = "vae2_conv2d_bwd_weight";
+  VAE2_REQUIRE(xd && dw_ld >= xd->c * k * k, fn, "bad dW row stride");
   VAE2_REQUIRE(x && dy && dw && ws, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(xd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
   VAE2_REQUIRE(fits32(xd) && fits32(dyd), fn, "tensor too large for 32-bit indexing");
@@ -1376,7 +1386,7 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
 reduce:
   int64_t slab = dyd->c * (int64_t)ncol4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 64)), dim3(256), 0, s,
-                     (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw,
+                     (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw, dw_ld,
                      accumulate);
   int rc = check_launch(fn);
   if (rc) return rc;
@@ -1392,6 +1402,15 @@ reduce:
     if (rc) return rc;
   }
   return 0;
+}
+
+int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
+                           const vae2_act* dyd, float* dw, float* dbias, int k,
+                           int stride, int pad, int accumulate, float* ws,
+                           int64_t ws_size, void* stream) {
+  if (!xd) return fail("vae2_conv2d_bwd_weight", "null descriptor");
+  return vae2_conv2d_bwd_weight_ld(x, xd, dy, dyd, dw, xd->c * k * k, dbias, k, stride, pad,
+                                   accumulate, ws, ws_size, stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,702 @@
+// Output stage of the HRNet heads: BatchNorm-apply + ReLU + the final narrow 1x1 conv
+// (270 -> NUM_CLASSES), forward and backward, without materialising the ReLU output.
+//
+//   last_layer = Conv1x1(C->C, bias) -> BatchNorm2d -> ReLU -> Conv1x1(C->CO, bias)
+//   (enc_hrnet.py:323-370 / :598-750; applied at :839-847, :897-905, :955-963)
+//
+// The wide 1x1 conv itself runs per branch (vae2_conv2d_fwd at the branch resolution,
+// then upsum_kernel below: full-resolution block + upsampled branch terms + bias + BN
+// statistics); the output-stage kernels take its pre-BN output y, the BN coefficients and
+//   forward   out[p][o] = b2[o] + sum_c w2[o][c] * relu(y[p][c]*scale[c] + shift[c])
+//   backward  g[p][c]  = (sum_o w2[o][c] * dout[p][o]) * [h > 0]      (h = ReLU input)
+//             reduce:  sum_p g, sum_p g*xhat (BN backward sums), dW2, db2
+//             apply:   dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)), sum_p dy (conv bias)
+// Each pass reads y once (16-byte NHWC quads); h and g are recomputed in registers.
+// Reductions are two-level with fixed orders (deterministic).
+#include "common.h"
+
+namespace vae2 {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kHeadMaxOut = 4;
+
+__device__ __forceinline__ f4 hld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+__device__ __forceinline__ f4 hchan4(const float* a, int c, int C) {
+  f4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = (c + k < C) ? a[c + k] : 0.f;
+  return v;
+}
+
+// Forward: 16 lanes per pixel (lane l takes channel quads l, l+16, ...), 16 pixels per
+// block pass; the per-channel coefficients and W2 live in LDS as quads.
+template <int CO>
+__global__ __launch_bounds__(256) void head_out_fwd_kernel(
+    const float* __restrict__ y, Act yd, const float* __restrict__ save,
+    const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ out,
+    Act od) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int C = (int)yd.c, c4 = (C + 3) >> 2;
+  f4* ssc = reinterpret_cast<f4*>(hsm);
+  f4* ssh = ssc + c4;
+  f4* sw = ssh + c4;  // [CO][c4]
+  for (int q = threadIdx.x; q < c4; q += 256) {
+    ssc[q] = hchan4(save + 2 * C, 4 * q, C);
+    ssh[q] = hchan4(save + 3 * C, 4 * q, C);
+#pragma unroll
+    for (int o = 0; o < CO; ++o) sw[o * c4 + q] = hchan4(w2 + (int64_t)o * C, 4 * q, C);
+  }
+  __syncthreads();
+  const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t P = yd.n * yd.h * yd.w;
+  for (int64_t p = (int64_t)blockIdx.x * 16 + grp; p < P; p += (int64_t)gridDim.x * 16) {
+    float acc[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    const float* yp = y + p * yd.ps;
+    for (int q = l; q < c4; q += 16) {
+      const f4 v = hld4(yp + 4 * q);
+      const f4 a = ssc[q], b = ssh[q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float h = __builtin_fmaf(v[k], a[k], b[k]);
+        h = (4 * q + k < C && h > 0.f) ? h : 0.f;
+#pragma unroll
+        for (int o = 0; o < CO; ++o) acc[o] += h * sw[o * c4 + q][k];
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      acc[o] += __shfl_xor(acc[o], 8, 16);
+      acc[o] += __shfl_xor(acc[o], 4, 16);
+      acc[o] += __shfl_xor(acc[o], 2, 16);
+      acc[o] += __shfl_xor(acc[o], 1, 16);
+    }
+    if (l == 0) {
+#pragma unroll
+      for (int o = 0; o < CO; ++o) out[p * od.ps + o] = acc[o] + (b2 ? b2[o] : 0.f);
+    }
+  }
+}
+
+// Per-thread state of the backward passes: thread (r, q) owns channels 4q..4q+3 and
+// walks pixels p0 + r, p0 + r + rows, ... of its block's pixel range.
+struct HeadCoef {
+  f4 mean, invstd, sc, sh;
+};
+
+__device__ __forceinline__ HeadCoef head_coef(const float* save, int c, int C) {
+  HeadCoef h;
+  h.mean = hchan4(save, c, C);
+  h.invstd = hchan4(save + C, c, C);
+  h.sc = hchan4(save + 2 * C, c, C);
+  h.sh = hchan4(save + 3 * C, c, C);
+  return h;
+}
+
+// Partial-row columns: [0,C) sum g | [C,2C) sum g*xhat | [2C, 2C+CO*C) dW2[o][c] | CO x db2
+template <int CO>
+__global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
+    const float* __restrict__ y, Act yd, const float* __restrict__ save,
+    const float* __restrict__ w2, const float* __restrict__ dout, Act dod, int64_t ppb,
+    int rows, float* __restrict__ part) {
+  extern __shared__ float red[];  // [rows][NC]
+  const int C = (int)yd.c, c4 = (C + 3) >> 2;
+  const int NC = 2 * C + CO * C + CO;
+  const int tid = threadIdx.x;
+  const int64_t P = yd.n * yd.h * yd.w;
+  const int64_t p0 = blockIdx.x * ppb;
+  const int64_t p1 = p0 + ppb < P ? p0 + ppb : P;
+  const int r = tid / c4, q = tid - r * c4, c = 4 * q;
+  if (tid < rows * c4) {
+    const HeadCoef hc = head_coef(save, c, C);
+    f4 wv[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) wv[o] = hchan4(w2 + (int64_t)o * C, c, C);
+    f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    f4 dw[CO];
+    float db[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) { dw[o] = s0; db[o] = 0.f; }
+    for (int64_t p = p0 + r; p < p1; p += rows) {
+      const f4 v = hld4(y + p * yd.ps + c);
+      float d[CO];
+#pragma unroll
+      for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
+        const bool m = h > 0.f;
+        h = m ? h : 0.f;
+        float dh = 0.f;
+#pragma unroll
+        for (int o = 0; o < CO; ++o) dh += wv[o][k] * d[o];
+        const float g = m ? dh : 0.f;
+        s0[k] += g;
+        s1[k] += g * (v[k] - hc.mean[k]) * hc.invstd[k];
+#pragma unroll
+        for (int o = 0; o < CO; ++o) dw[o][k] += d[o] * h;
+      }
+#pragma unroll
+      for (int o = 0; o < CO; ++o) db[o] += d[o];
+    }
+    float* rr = red + r * NC;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (c + k >= C) break;
+      rr[c + k] = s0[k];
+      rr[C + c + k] = s1[k];
+#pragma unroll
+      for (int o = 0; o < CO; ++o) rr[2 * C + o * C + c + k] = dw[o][k];
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int o = 0; o < CO; ++o) rr[2 * C + CO * C + o] = db[o];
+    }
+  }
+  __syncthreads();
+  for (int col = tid; col < NC; col += 256) {
+    float a = 0.f;
+    for (int i = 0; i < rows; ++i) a += red[i * NC + col];
+    part[(int64_t)blockIdx.x * NC + col] = a;
+  }
+}
+
+// Column sums of the reduce partials (coalesced: lane = column, 4 waves over rows in
+// double, combined in a fixed order) routed to their destinations.
+__global__ __launch_bounds__(256) void head_bwd_colsum_kernel(
+    const float* __restrict__ part, int nrows, int C, int CO, double* __restrict__ sums,
+    float* dgamma, float* dbeta, float* dw2, float* db2) {
+  __shared__ double red[4][64];
+  const int NC = 2 * C + CO * C + CO;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (col < NC)
+    for (int i = wave; i < nrows; i += 4) s += (double)part[(int64_t)i * NC + col];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || col >= NC) return;
+  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  if (col < C) {
+    sums[col] = s;
+    if (dbeta) dbeta[col] += (float)s;
+  } else if (col < 2 * C) {
+    sums[col] = s;
+    if (dgamma) dgamma[col - C] += (float)s;
+  } else if (col < 2 * C + CO * C) {
+    if (dw2) dw2[col - 2 * C] += (float)s;
+  } else {
+    if (db2) db2[col - 2 * C - CO * C] += (float)s;
+  }
+}
+
+// dy = gamma*invstd*(g - sum_g/count - xhat*sum_gxhat/count); partial rows [block][C]
+// of sum_p dy (the wide conv's bias gradient).
+template <int CO>
+__global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
+    const float* __restrict__ y, Act yd, const float* __restrict__ save,
+    const float* __restrict__ gamma, const float* __restrict__ w2,
+    const float* __restrict__ dout, Act dod, const double* __restrict__ sums, double count,
+    int64_t ppb, int rows, float* __restrict__ dy, Act dyd, float* __restrict__ part) {
+  extern __shared__ float red[];  // [rows][C]
+  const int C = (int)yd.c, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  const int64_t P = yd.n * yd.h * yd.w;
+  const int64_t p0 = blockIdx.x * ppb;
+  const int64_t p1 = p0 + ppb < P ? p0 + ppb : P;
+  const int r = tid / c4, q = tid - r * c4, c = 4 * q;
+  if (tid < rows * c4) {
+    const HeadCoef hc = head_coef(save, c, C);
+    const float inv_n = (float)(1.0 / count);
+    f4 wv[CO], mg, mgx, k4;
+#pragma unroll
+    for (int o = 0; o < CO; ++o) wv[o] = hchan4(w2 + (int64_t)o * C, c, C);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int ch = c + k < C ? c + k : C - 1;
+      mg[k] = (float)sums[ch] * inv_n;
+      mgx[k] = (float)sums[C + ch] * inv_n;
+      k4[k] = (gamma ? gamma[ch] : 1.f) * hc.invstd[k];
+    }
+    f4 sdy = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t p = p0 + r; p < p1; p += rows) {
+      const f4 v = hld4(y + p * yd.ps + c);
+      float d[CO];
+#pragma unroll
+      for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
+      f4 o4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
+        float dh = 0.f;
+#pragma unroll
+        for (int o = 0; o < CO; ++o) dh += wv[o][k] * d[o];
+        const float g = h > 0.f ? dh : 0.f;
+        const float xh = (v[k] - hc.mean[k]) * hc.invstd[k];
+        o4[k] = k4[k] * (g - mg[k] - xh * mgx[k]);
+        sdy[k] += o4[k];
+      }
+      float* dst = dy + p * dyd.ps + c;
+      if (c + 4 <= C) {
+        *reinterpret_cast<f4*>(dst) = o4;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c + k < C) dst[k] = o4[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < C) red[r * C + c + k] = sdy[k];
+  }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    float a = 0.f;
+    for (int i = 0; i < rows; ++i) a += red[i * C + ch];
+    part[(int64_t)blockIdx.x * C + ch] = a;
+  }
+}
+
+// ------------------------------------------------------------------ up-sum ----
+// y[n,oy,x,c] = sum_k x0[n,oy,x,k] w[c][k] + sum_s up(z_s)[n,oy,x,c] + bias[c]
+// (the wide head conv split by branch; z_s = W_s y_s at the branch resolution).
+// Workgroup = (image row, 64-pixel chunk, 64-channel block), lane = channel, W0 column
+// in registers.  Staged in LDS once per workgroup: the chunk's x0 pixels (16-byte
+// rows), each source's two contributing rows blended vertically over the chunk's
+// source-column window, and per-pixel horizontal interpolation tables; every output
+// pixel then costs ceil(cin/4) + 3 broadcast reads, 2 reads per source and cin + 2*nup
+// FMAs.  Coalesced 256-byte NHWC segments in and out; BN partial sums per (row, chunk).
+constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32;
+
+struct UpSum {
+  const float* x;
+  int x_ps, cin, cin4, H, W;
+  const float* w;
+  int w_ld;
+  const float* bias;
+  const float* z[3];
+  int zh[3], zw[3], zps[3];
+  float sh[3], sw[3];
+  int vcols;
+  float* y;
+  int y_ps, C;
+  float* stats;  // [2][rows][C], row = (n*H + oy)*nxb + xb
+  int rows, nxb;
+};
+
+template <int NUP>
+__global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
+  extern __shared__ __attribute__((aligned(16))) float usm[];
+  __shared__ float red[2][4][kUsCB];
+  f4* tab = reinterpret_cast<f4*>(usm);                  // [NUP][kUsXB] {i0, i1, l0, l1}
+  float* xs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [kUsXB][cin4]
+  float* vs = xs + kUsXB * p.cin4;                        // [NUP][vcols][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x;
+  const int n = row / p.H, oy = row - n * p.H;
+  const int xb = blockIdx.y, x0 = xb * kUsXB;
+  const int c = blockIdx.z * kUsCB + lane;
+  const bool cok = c < p.C;
+  const int xn = p.W - x0 < kUsXB ? p.W - x0 : kUsXB;
+  float wreg[kUsMaxCin];
+#pragma unroll
+  for (int k = 0; k < kUsMaxCin; ++k)
+    wreg[k] = (k < p.cin && cok) ? p.w[(int64_t)c * p.w_ld + k] : 0.f;
+  const float* xrow = p.x + ((int64_t)row * p.W + x0) * p.x_ps;
+  for (int i = threadIdx.x; i < xn * p.cin4; i += 256) {
+    const int px = i / p.cin4, k = i - px * p.cin4;
+    xs[i] = k < p.cin ? xrow[(int64_t)px * p.x_ps + k] : 0.f;
+  }
+  int vlo[3] = {0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+    vlo[s] = lerp_index(x0, p.zw[s], p.sw[s]).i0;
+    const int hi = lerp_index(x0 + xn - 1, p.zw[s], p.sw[s]).i1;
+    if (threadIdx.x < xn) {
+      const Lerp lx = lerp_index(x0 + threadIdx.x, p.zw[s], p.sw[s]);
+      tab[s * kUsXB + threadIdx.x] =
+          f4{__int_as_float(lx.i0 - vlo[s]), __int_as_float(lx.i1 - vlo[s]), lx.l0, lx.l1};
+    }
+    const Lerp ly = lerp_index(oy, p.zh[s], p.sh[s]);
+    const int64_t ibase = (int64_t)n * p.zh[s];
+    const float* r0 = p.z[s] + (ibase + ly.i0) * p.zw[s] * p.zps[s] + c;
+    const float* r1 = p.z[s] + (ibase + ly.i1) * p.zw[s] * p.zps[s] + c;
+    for (int ix = vlo[s] + wave; ix <= hi; ix += 4) {
+      float v = 0.f;
+      if (cok) v = ly.l0 * r0[(int64_t)ix * p.zps[s]] + ly.l1 * r1[(int64_t)ix * p.zps[s]];
+      vs[(s * p.vcols + (ix - vlo[s])) * kUsCB + lane] = v;
+    }
+  }
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  const float b = (p.bias && cok) ? p.bias[c] : 0.f;
+  float* yout = p.y + ((int64_t)row * p.W + x0) * p.y_ps + c;
+  for (int px = wave; px < xn; px += 4) {
+    float acc = 0.f;
+    const f4* xq = reinterpret_cast<const f4*>(xs + px * p.cin4);
+#pragma unroll
+    for (int q = 0; q < kUsMaxCin / 4; ++q) {
+      if (4 * q < p.cin) {
+        const f4 xv = xq[q];
+        acc = __builtin_fmaf(xv[0], wreg[4 * q], acc);
+        acc = __builtin_fmaf(xv[1], wreg[4 * q + 1], acc);
+        acc = __builtin_fmaf(xv[2], wreg[4 * q + 2], acc);
+        acc = __builtin_fmaf(xv[3], wreg[4 * q + 3], acc);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NUP; ++s) {
+      const f4 t = tab[s * kUsXB + px];
+      const float* v = vs + s * p.vcols * kUsCB + lane;
+      acc += t[2] * v[__float_as_int(t[0]) * kUsCB] + t[3] * v[__float_as_int(t[1]) * kUsCB];
+    }
+    const float o = acc + b;
+    if (cok) {
+      yout[(int64_t)px * p.y_ps] = o;
+      s1 += o;
+      s2 += o * o;
+    }
+  }
+  if (p.stats) {
+    red[0][wave][lane] = s1;
+    red[1][wave][lane] = s2;
+    __syncthreads();
+    if (wave == 0 && cok) {
+      const int r = row * p.nxb + xb;
+      p.stats[(int64_t)r * p.C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] +
+                                      red[0][3][lane];
+      p.stats[((int64_t)p.rows + r) * p.C + c] = red[1][0][lane] + red[1][1][lane] +
+                                                 red[1][2][lane] + red[1][3][lane];
+    }
+  }
+}
+
+// ------------------------------------------- upsampling adjoint, all sources ----
+// dx_s = up_s^T(dy) for every source s at once, separably.
+// Horizontal pass, workgroup = (dY row, 64-pixel chunk, 64-channel block): source
+// columns are partitioned between chunks (ix belongs to the chunk holding the output
+// coordinate of its centre), the chunk's dY pixels plus the interpolation halo are
+// staged in LDS once with per-pixel forward tables {i0, i1, l0, l1}, and each owned
+// column gathers hb_s[n][oy][ix][c] = sum_ox w(ox, ix) dy[n][oy][ox][c] from LDS.
+// Vertical pass, workgroup = (target row, 64-channel block): the row's weights are
+// tabulated once, then dx_s[n][iy][ix][c] = sum_oy w(oy, iy) hb_s[n][oy][ix][c].
+// The weights are exactly upsample_fwd_kernel's (lerp_index).  Lane = channel.
+struct UpAdj {
+  const float* dy;
+  int dy_ps, H, W, C;
+  float* hb[3];
+  float* dx[3];
+  int zh[3], zw[3], dx_ps[3];
+  float sh[3], sw[3];
+  int halo, nxb;
+};
+
+__device__ __forceinline__ void adj_window(int i, int in_size, int out_size, float scale,
+                                           int& lo, int& hi) {
+  lo = (int)floorf(((float)i - 0.5f) / scale - 0.5f) - 1;
+  hi = (int)ceilf(((float)i + 1.5f) / scale - 0.5f) + 1;
+  if (lo < 0) lo = 0;
+  if (hi > out_size - 1) hi = out_size - 1;
+  if (i == in_size - 1) hi = out_size - 1;  // clamped sources beyond the last input
+}
+
+// First source column owned by chunk xb (monotone in xb; xb = nxb gives zw).
+__device__ __forceinline__ int adj_owned_begin(int xb, int nxb, int zw, float sw) {
+  if (xb >= nxb) return zw;
+  if (xb <= 0) return 0;
+  int b = (int)ceilf(((float)(xb * kUsXB) + 0.5f) * sw - 0.5f);
+  return b < 0 ? 0 : (b > zw ? zw : b);
+}
+
+template <int NUP>
+__global__ __launch_bounds__(256) void up_adj_h_kernel(UpAdj p) {
+  extern __shared__ __attribute__((aligned(16))) float asm_[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x;  // n*H + oy
+  const int xb = blockIdx.y;
+  const int c = blockIdx.z * 64 + lane;
+  const bool cok = c < p.C;
+  const int span = kUsXB + 2 * p.halo;
+  f4* tab = reinterpret_cast<f4*>(asm_);              // [NUP][span]
+  float* st = asm_ + 4 * NUP * span;                  // [span][64]
+  int ib[3], ie[3], wlo = 1 << 30, whi = -1;
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+    ib[s] = adj_owned_begin(xb, p.nxb, p.zw[s], p.sw[s]);
+    ie[s] = adj_owned_begin(xb + 1, p.nxb, p.zw[s], p.sw[s]);
+    if (ie[s] > ib[s]) {
+      int lo, hi, lo2, hi2;
+      adj_window(ib[s], p.zw[s], p.W, p.sw[s], lo, hi);
+      adj_window(ie[s] - 1, p.zw[s], p.W, p.sw[s], lo2, hi2);
+      wlo = lo < wlo ? lo : wlo;
+      whi = hi2 > whi ? hi2 : whi;
+    }
+  }
+  if (whi < wlo) return;  // no owned columns (uniform over the workgroup)
+  const int cnt = whi - wlo + 1;  // <= span (host-sized halo)
+  const float* drow = p.dy + (int64_t)row * p.W * p.dy_ps + c;
+  for (int i = wave; i < cnt; i += 4) st[i * 64 + lane] = cok ? drow[(int64_t)(wlo + i) * p.dy_ps] : 0.f;
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+      const Lerp lx = lerp_index(wlo + i, p.zw[s], p.sw[s]);
+      tab[s * span + i] = f4{__int_as_float(lx.i0), __int_as_float(lx.i1), lx.l0, lx.l1};
+    }
+  }
+  __syncthreads();
+  if (!cok) return;
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+    float* hrow = p.hb[s] + (int64_t)row * p.zw[s] * p.C + c;
+    for (int ix = ib[s] + wave; ix < ie[s]; ix += 4) {
+      int lo, hi;
+      adj_window(ix, p.zw[s], p.W, p.sw[s], lo, hi);
+      float acc = 0.f;
+      for (int ox = lo; ox <= hi; ++ox) {
+        const f4 t = tab[s * span + (ox - wlo)];
+        const float w = (__float_as_int(t[0]) == ix ? t[2] : 0.f) +
+                        (__float_as_int(t[1]) == ix ? t[3] : 0.f);
+        acc = __builtin_fmaf(w, st[(ox - wlo) * 64 + lane], acc);
+      }
+      hrow[(int64_t)ix * p.C] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void up_adj_v_kernel(UpAdj p, int s) {
+  __shared__ float wy[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x;  // n*zh + iy
+  const int n = row / p.zh[s], iy = row - n * p.zh[s];
+  const int c = blockIdx.y * 64 + lane;
+  int lo, hi;
+  adj_window(iy, p.zh[s], p.H, p.sh[s], lo, hi);
+  const int cnt = hi - lo + 1 < 64 ? hi - lo + 1 : 64;  // host guarantees <= 64
+  if (threadIdx.x < cnt) {
+    const Lerp ly = lerp_index(lo + threadIdx.x, p.zh[s], p.sh[s]);
+    wy[threadIdx.x] = (ly.i0 == iy ? ly.l0 : 0.f) + (ly.i1 == iy ? ly.l1 : 0.f);
+  }
+  __syncthreads();
+  if (c >= p.C) return;
+  const float* hb = p.hb[s] + ((int64_t)n * p.H + lo) * p.zw[s] * p.C + c;
+  float* out = p.dx[s] + (int64_t)row * p.zw[s] * p.dx_ps[s] + c;
+  const int64_t rs = (int64_t)p.zw[s] * p.C;
+  for (int ix = wave; ix < p.zw[s]; ix += 4) {
+    float acc = 0.f;
+    for (int t = 0; t < cnt; ++t) acc = __builtin_fmaf(wy[t], hb[t * rs + (int64_t)ix * p.C], acc);
+    out[(int64_t)ix * p.dx_ps[s]] = acc;
+  }
+}
+
+// Pixels per block of the backward passes (<= 1024 blocks, >= 64 pixels each).
+static int64_t head_ppb(int64_t P) {
+  int64_t ppb = ceil_div(P, 1024);
+  return ppb < 64 ? 64 : ppb;
+}
+
+static bool head_args_ok(const float* y, const vae2_act* yd, int cout2) {
+  return y && act_ok(yd) && ((uintptr_t)y % 16 == 0) && yd->ps % 4 == 0 &&
+         (yd->c + 3) / 4 <= 256 && cout2 >= 1 && cout2 <= kHeadMaxOut;
+}
+
+#define HEAD_DISPATCH(CO_, KERNEL, ...)                                   \
+  switch (CO_) {                                                          \
+    case 1: hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); break;          \
+    case 2: hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__); break;          \
+    case 3: hipLaunchKernelGGL((KERNEL<3>), __VA_ARGS__); break;          \
+    default: hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__); break;         \
+  }
+
+}  // namespace vae2
+
+using namespace vae2;
+
+extern "C" {
+
+int vae2_head_out_fwd(const float* y, const vae2_act* yd, const float* save, const float* w2,
+                      const float* b2, int cout2, float* out, const vae2_act* outd,
+                      void* stream) {
+  const char* fn = "vae2_head_out_fwd";
+  VAE2_REQUIRE(head_args_ok(y, yd, cout2) && save && w2 && out && act_ok(outd), fn,
+               "bad arguments (y must be 16-byte aligned NHWC with ps % 4 == 0, cout2 <= 4)");
+  VAE2_REQUIRE(outd->n == yd->n && outd->h == yd->h && outd->w == yd->w && outd->c >= cout2,
+               fn, "output shape mismatch");
+  const int c4 = (int)((yd->c + 3) / 4);
+  const size_t shm = (size_t)(2 + cout2) * c4 * 16;
+  const int64_t P = act_pixels(yd);
+  const unsigned grid = (unsigned)(ceil_div(P, 16) < 8192 ? ceil_div(P, 16) : 8192);
+  HEAD_DISPATCH(cout2, head_out_fwd_kernel, dim3(grid), dim3(256), shm, as_stream(stream), y,
+                to_act(yd), save, w2, b2, out, to_act(outd));
+  return check_launch(fn);
+}
+
+int64_t vae2_head_out_bwd_ws_size(const vae2_act* yd, int cout2) {
+  if (!act_ok(yd)) return 0;
+  const int64_t P = act_pixels(yd);
+  const int64_t blocks = ceil_div(P, head_ppb(P));
+  const int64_t NC = 2 * yd->c + cout2 * yd->c + cout2;
+  return blocks * NC;
+}
+
+int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* save,
+                             const float* w2, int cout2, const float* dout,
+                             const vae2_act* doutd, double* sums, float* dgamma, float* dbeta,
+                             float* dw2, float* db2, float* ws, int64_t ws_size, void* stream) {
+  const char* fn = "vae2_head_out_bwd_reduce";
+  VAE2_REQUIRE(head_args_ok(y, yd, cout2) && save && w2 && dout && sums && ws &&
+                   act_ok(doutd), fn, "bad arguments");
+  VAE2_REQUIRE(doutd->n == yd->n && doutd->h == yd->h && doutd->w == yd->w &&
+                   doutd->c >= cout2, fn, "dout shape mismatch");
+  VAE2_REQUIRE(ws_size >= vae2_head_out_bwd_ws_size(yd, cout2), fn, "workspace too small");
+  const int C = (int)yd->c, c4 = (C + 3) / 4, rows = 256 / c4;
+  const int NC = 2 * C + cout2 * C + cout2;
+  const int64_t P = act_pixels(yd), ppb = head_ppb(P);
+  const unsigned blocks = (unsigned)ceil_div(P, ppb);
+  const size_t shm = (size_t)rows * NC * sizeof(float);
+  VAE2_REQUIRE(shm <= 64 * 1024, fn, "too many channels for the LDS reduction");
+  HEAD_DISPATCH(cout2, head_out_bwd_reduce_kernel, dim3(blocks), dim3(256), shm,
+                as_stream(stream), y, to_act(yd), save, w2, dout, to_act(doutd), ppb, rows, ws);
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  hipLaunchKernelGGL(head_bwd_colsum_kernel, dim3((unsigned)ceil_div(NC, 64)), dim3(256), 0,
+                     as_stream(stream), (const float*)ws, (int)blocks, C, cout2, sums, dgamma,
+                     dbeta, dw2, db2);
+  return check_launch(fn);
+}
+
+int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* save,
+                            const float* gamma, const float* w2, int cout2, const float* dout,
+                            const vae2_act* doutd, const double* sums, double count, float* dy,
+                            const vae2_act* dyd, float* dbias, float* ws, int64_t ws_size,
+                            void* stream) {
+  const char* fn = "vae2_head_out_bwd_apply";
+  VAE2_REQUIRE(head_args_ok(y, yd, cout2) && save && w2 && dout && sums && dy && ws &&
+                   act_ok(doutd) && act_ok(dyd) && count > 0, fn, "bad arguments");
+  VAE2_REQUIRE(doutd->n == yd->n && doutd->h == yd->h && doutd->w == yd->w &&
+                   doutd->c >= cout2, fn, "dout shape mismatch");
+  VAE2_REQUIRE(dyd->n == yd->n && dyd->h == yd->h && dyd->w == yd->w && dyd->c == yd->c &&
+                   ((uintptr_t)dy % 16 == 0) && dyd->ps % 4 == 0, fn, "dy shape mismatch");
+  VAE2_REQUIRE(ws_size >= vae2_head_out_bwd_ws_size(yd, cout2), fn, "workspace too small");
+  const int C = (int)yd->c, c4 = (C + 3) / 4, rows = 256 / c4;
+  const int64_t P = act_pixels(yd), ppb = head_ppb(P);
+  const unsigned blocks = (unsigned)ceil_div(P, ppb);
+  const size_t shm = (size_t)rows * C * sizeof(float);
+  HEAD_DISPATCH(cout2, head_out_bwd_apply_kernel, dim3(blocks), dim3(256), shm,
+                as_stream(stream), y, to_act(yd), save, gamma, w2, dout, to_act(doutd), sums,
+                count, ppb, rows, dy, to_act(dyd), ws);
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  if (dbias) return bias_grad_from_partials(ws, blocks, C, dbias, 1, stream);
+  return 0;
+}
+
+int64_t vae2_conv1x1_upsum_stats_rows(const vae2_act* yd) {
+  if (!act_ok(yd)) return 0;
+  return yd->n * yd->h * ceil_div(yd->w, kUsXB);
+}
+
+int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, int64_t w_ld,
+                           const float* bias, int nup, const float* const* ups,
+                           const vae2_act* upds, float* y, const vae2_act* yd, float* stats,
+                           void* stream) {
+  const char* fn = "vae2_conv1x1_upsum_fwd";
+  VAE2_REQUIRE(x && w && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(xd->n == yd->n && xd->h == yd->h && xd->w == yd->w, fn, "x / y shape mismatch");
+  VAE2_REQUIRE(w_ld >= xd->c && xd->c <= kUsMaxCin, fn, "bad weight block (Cin0 <= 32)");
+  VAE2_REQUIRE(nup >= 0 && nup <= 3 && (nup == 0 || (ups && upds)), fn, "bad up-sum terms");
+  UpSum p{};
+  p.x = x; p.x_ps = (int)xd->ps; p.cin = (int)xd->c; p.cin4 = ((int)xd->c + 3) / 4 * 4;
+  p.H = (int)yd->h; p.W = (int)yd->w;
+  p.w = w; p.w_ld = (int)w_ld; p.bias = bias;
+  int vcols = 1;
+  for (int s = 0; s < nup; ++s) {
+    const vae2_act* u = &upds[s];
+    VAE2_REQUIRE(ups[s] && act_ok(u) && u->n == yd->n && u->c >= yd->c && u->h <= yd->h &&
+                     u->w <= yd->w, fn, "up-sum term shape mismatch");
+    p.z[s] = ups[s]; p.zh[s] = (int)u->h; p.zw[s] = (int)u->w; p.zps[s] = (int)u->ps;
+    p.sh[s] = (float)u->h / (float)yd->h;
+    p.sw[s] = (float)u->w / (float)yd->w;
+    const int vc = (int)ceilf(p.sw[s] * kUsXB) + 3;
+    if (vc > vcols) vcols = vc;
+  }
+  p.vcols = vcols;
+  p.y = y; p.y_ps = (int)yd->ps; p.C = (int)yd->c;
+  p.stats = stats;
+  p.nxb = (int)ceil_div(yd->w, kUsXB);
+  p.rows = (int)vae2_conv1x1_upsum_stats_rows(yd);
+  const int nu = nup > 0 ? nup : 1;
+  const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)kUsXB * p.cin4 +
+                      (size_t)nu * vcols * kUsCB) * sizeof(float);
+  dim3 grid((unsigned)(yd->n * yd->h), (unsigned)p.nxb, (unsigned)ceil_div(yd->c, kUsCB));
+  hipStream_t st = as_stream(stream);
+  switch (nup) {
+    case 0: hipLaunchKernelGGL(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
+    case 1: hipLaunchKernelGGL(upsum_kernel<1>, grid, dim3(256), shm, st, p); break;
+    case 2: hipLaunchKernelGGL(upsum_kernel<2>, grid, dim3(256), shm, st, p); break;
+    default: hipLaunchKernelGGL(upsum_kernel<3>, grid, dim3(256), shm, st, p); break;
+  }
+  return check_launch(fn);
+}
+
+int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
+                                                 const vae2_act* dxds) {
+  if (!act_ok(dyd) || n < 0 || n > 3 || (n && !dxds)) return 0;
+  int64_t t = 0;
+  for (int s = 0; s < n; ++s) t += dyd->n * dyd->h * dxds[s].w * dyd->c;
+  return t > 0 ? t : 1;
+}
+
+int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n,
+                                     float* const* dxs, const vae2_act* dxds, float* ws,
+                                     int64_t ws_size, void* stream) {
+  const char* fn = "vae2_upsample_bilinear_bwd_multi";
+  VAE2_REQUIRE(dy && act_ok(dyd) && n >= 0 && n <= 3 && (n == 0 || (dxs && dxds)) && ws, fn,
+               "bad arguments");
+  VAE2_REQUIRE(ws_size >= vae2_upsample_bilinear_bwd_multi_ws_size(dyd, n, dxds), fn,
+               "workspace too small");
+  if (n == 0) return 0;
+  UpAdj p{};
+  p.dy = dy; p.dy_ps = (int)dyd->ps; p.H = (int)dyd->h; p.W = (int)dyd->w; p.C = (int)dyd->c;
+  float* hb = ws;
+  float min_sw = 1.f;
+  for (int s = 0; s < n; ++s) {
+    const vae2_act* d = &dxds[s];
+    VAE2_REQUIRE(dxs[s] && act_ok(d) && d->n == dyd->n && d->c == dyd->c && d->h <= dyd->h &&
+                     d->w <= dyd->w, fn, "dx shape mismatch");
+    p.dx[s] = dxs[s]; p.zh[s] = (int)d->h; p.zw[s] = (int)d->w; p.dx_ps[s] = (int)d->ps;
+    p.sh[s] = (float)d->h / (float)dyd->h;
+    p.sw[s] = (float)d->w / (float)dyd->w;
+    VAE2_REQUIRE(2.f / p.sh[s] + 6.f <= 64.f, fn, "upsampling ratio too large (> 24)");
+    if (p.sw[s] < min_sw) min_sw = p.sw[s];
+    p.hb[s] = hb;
+    hb += dyd->n * dyd->h * d->w * dyd->c;
+  }
+  // halo: the owned columns' windows reach at most 1/sw + 3 pixels past the chunk
+  p.halo = (int)ceilf(1.f / min_sw) + 4;
+  p.nxb = (int)ceil_div(dyd->w, kUsXB);
+  const unsigned cb = (unsigned)ceil_div(dyd->c, 64);
+  const int span = kUsXB + 2 * p.halo;
+  const size_t shm = (size_t)(4 * n + 64) * span * sizeof(float);
+  VAE2_REQUIRE(shm <= 64 * 1024, fn, "upsampling ratio too large for the LDS tile");
+  dim3 grid((unsigned)(dyd->n * dyd->h), (unsigned)p.nxb, cb);
+  hipStream_t st = as_stream(stream);
+  switch (n) {
+    case 1: hipLaunchKernelGGL(up_adj_h_kernel<1>, grid, dim3(256), shm, st, p); break;
+    case 2: hipLaunchKernelGGL(up_adj_h_kernel<2>, grid, dim3(256), shm, st, p); break;
+    default: hipLaunchKernelGGL(up_adj_h_kernel<3>, grid, dim3(256), shm, st, p); break;
+  }
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  for (int s = 0; s < n; ++s) {
+    hipLaunchKernelGGL(up_adj_v_kernel, dim3((unsigned)(dyd->n * p.zh[s]), cb), dim3(256), 0, st,
+                       p, s);
+    rc = check_launch(fn);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+}  // extern "C"

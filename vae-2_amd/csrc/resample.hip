@@ -32,26 +32,7 @@ int check_launch(const char* fn) {
 }
 
 // ------------------------------------------------- bilinear helpers ----
-// PyTorch's area_pixel_compute_source_index for align_corners=False, in fp32.
-struct Lerp {
-  int i0, i1;
-  float l0, l1;
-};
-
-__device__ __forceinline__ Lerp lerp_index(int dst, int in_size, float scale) {
-  float src = scale * ((float)dst + 0.5f) - 0.5f;
-  if (src < 0.f) src = 0.f;
-  int i0 = (int)src;
-  if (i0 > in_size - 1) i0 = in_size - 1;
-  int ip = (i0 < in_size - 1) ? 1 : 0;
-  Lerp l;
-  l.i0 = i0;
-  l.i1 = i0 + ip;
-  l.l1 = src - (float)i0;
-  l.l0 = 1.f - l.l1;
-  return l;
-}
-
+// (lerp_index: common.h)
 __device__ __forceinline__ float bilinear_at(const float* __restrict__ x, const Act& xd,
                                              int64_t n, int oy, int ox, int c, float sh,
                                              float sw) {
@@ -63,15 +44,6 @@ __device__ __forceinline__ float bilinear_at(const float* __restrict__ x, const 
   float x10 = base[((int64_t)ly.i1 * xd.w + lx.i0) * xd.ps];
   float x11 = base[((int64_t)ly.i1 * xd.w + lx.i1) * xd.ps];
   return ly.l0 * (lx.l0 * x00 + lx.l1 * x01) + ly.l1 * (lx.l0 * x10 + lx.l1 * x11);
-}
-
-// Weight with which output coordinate `o` reads input coordinate `i`.
-__device__ __forceinline__ float lerp_weight(int o, int in_size, float scale, int i) {
-  Lerp l = lerp_index(o, in_size, scale);
-  float w = 0.f;
-  if (l.i0 == i) w += l.l0;
-  if (l.i1 == i) w += l.l1;
-  return w;
 }
 
 __global__ __launch_bounds__(256) void upsample_fwd_kernel(const float* __restrict__ x, Act xd,

@@ -33,6 +33,7 @@ _SIGS = {
     "vae2_last_error": (ctypes.c_char_p, []),
     "vae2_conv2d_packed_size": (c_i64, [c_i64, c_i64, c_int, c_int]),
     "vae2_conv2d_pack_weight": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp]),
+    "vae2_conv2d_pack_weight_ld": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_i64, c_vp, c_vp]),
     "vae2_conv2d_pack_weights": (c_int, [c_vp, c_i64, c_vp]),
     "vae2_conv2d_fwd_stats_rows": (c_i64, [c_vp, P_ACT, P_ACT, c_int, c_int, c_int]),
     "vae2_conv2d_set_algo": (c_int, [c_int]),
@@ -45,6 +46,20 @@ _SIGS = {
     "vae2_conv2d_bwd_weight_ws_size": (c_i64, [P_ACT, P_ACT, c_int]),
     "vae2_conv2d_bwd_weight": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_vp, c_int, c_int,
                                        c_int, c_int, c_vp, c_i64, c_vp]),
+    "vae2_conv2d_bwd_weight_ld": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_i64, c_vp, c_int,
+                                          c_int, c_int, c_int, c_vp, c_i64, c_vp]),
+    "vae2_conv1x1_upsum_stats_rows": (c_i64, [P_ACT]),
+    "vae2_conv1x1_upsum_fwd": (c_int, [c_vp, P_ACT, c_vp, c_i64, c_vp, c_int, ctypes.POINTER(c_vp),
+                                       P_ACT, c_vp, P_ACT, c_vp, c_vp]),
+    "vae2_upsample_bilinear_bwd_multi_ws_size": (c_i64, [P_ACT, c_int, P_ACT]),
+    "vae2_upsample_bilinear_bwd_multi": (c_int, [c_vp, P_ACT, c_int, ctypes.POINTER(c_vp), P_ACT,
+                                                 c_vp, c_i64, c_vp]),
+    "vae2_head_out_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp]),
+    "vae2_head_out_bwd_ws_size": (c_i64, [P_ACT, c_int]),
+    "vae2_head_out_bwd_reduce": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "vae2_head_out_bwd_apply": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp,
+                                        c_f64, c_vp, P_ACT, c_vp, c_vp, c_i64, c_vp]),
     "vae2_bn_partial_rows": (c_i64, [P_ACT]),
     "vae2_bn_stats": (c_int, [c_vp, P_ACT, c_vp, c_vp]),
     "vae2_bn_partials_reduce": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_vp]),
@@ -90,7 +105,7 @@ _SIGS = {
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 
@@ -122,7 +137,8 @@ def exported_symbols():
 class PackJob(ctypes.Structure):
     """vae2_pack_job (include/vae2_hip.h)."""
     _fields_ = [("w", c_vp), ("out", c_vp), ("cout", ctypes.c_int32), ("cin", ctypes.c_int32),
-                ("k", ctypes.c_int32), ("mode", ctypes.c_int32)]
+                ("k", ctypes.c_int32), ("mode", ctypes.c_int32), ("ld", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
 
 
 class HipError(RuntimeError):

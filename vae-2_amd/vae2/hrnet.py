@@ -24,6 +24,7 @@ import os
 import torch
 import torch.nn as nn
 
+from . import heads as vheads
 from . import ops, streams
 
 BN_MOMENTUM = 0.01
@@ -300,6 +301,8 @@ class HighResolutionNet(nn.Module):
             setattr(self, f"last_layer_{k}", _head(self.last_inp_channels,
                                                    config.DATASET.NUM_CLASSES,
                                                    extra.FINAL_CONV_KERNEL))
+        vheads.mark_split([getattr(self, f"last_layer_{k}") for k in (1, 2, 3)],
+                          self.last_stage_channels)
 
     def _build_trunk(self, prefix, extra, code_extra):
         """layer1 .. stage4 under `prefix` (enc_hrnet.py:279-319 / :555-594)."""
@@ -360,6 +363,9 @@ class HighResolutionNet(nn.Module):
         return out
 
     def _heads(self, prefix, ys):
+        heads = [getattr(self, f"{prefix}last_layer_{k}") for k in (1, 2, 3)]
+        if vheads.supported(heads, [int(y.shape[3]) for y in ys]):
+            return vheads.run(heads, ys)  # per-branch 1x1 convs (vae2/heads.py)
         x = ops.up_cat(ys)
         outs = [run_head(getattr(self, f"{prefix}last_layer_{k}"), x) for k in (1, 2, 3)]
         return ops.cat(outs, x.shape[1:3])
@@ -419,6 +425,7 @@ class HighResolutionNetED(HighResolutionNet):
             for k in (1, 2, 3):
                 setattr(self, f"{d}last_layer_{k}", _head(nin, config.DATASET.NUM_CLASSES,
                                                           extra.FINAL_CONV_KERNEL))
+            vheads.mark_split([getattr(self, f"{d}last_layer_{k}") for k in (1, 2, 3)], pre)
 
     def _expand_pretrained(self, upd):
         L = self.clip_length

@@ -145,26 +145,38 @@ class PackPlan:
     """Every Conv2d weight of a module tree in both packed layouts, refreshed by one
     vae2_conv2d_pack_weights launch (FusedAdam calls run() after each update).
 
+    A conv carrying ``_vae2_col_split`` (a tuple of input-channel block widths: the
+    heads, whose 1x1 conv is computed per upsampled branch, vae2.heads) is packed
+    per input-channel block instead of whole.
+
     A weight's packed copy is used only while the weight is unchanged since the
     last run (same storage, same autograd version counter); otherwise the conv
     packs it itself, so in-place edits outside the optimizer stay correct."""
 
     def __init__(self, module):
         lib = _lib.load()
-        seen, self.weights = set(), []
+        seen, self.weights, self.splits = set(), [], []
         for m in module.modules():
             if isinstance(m, torch.nn.Conv2d) and id(m.weight) not in seen:
                 seen.add(id(m.weight))
                 self.weights.append(m.weight)
-        layout, total = [], 0
-        for w in self.weights:
+                self.splits.append(getattr(m, "_vae2_col_split", None))
+        self._blocks, total = [], 0  # per weight: [(c0, cin_block, off0, n0, off1, n1)]
+        for w, split in zip(self.weights, self.splits):
             cout, cin, k, _ = w.shape
-            sizes = [lib.vae2_conv2d_packed_size(cout, cin, k, mode) for mode in (0, 1)]
-            layout.append((total, sizes[0], total + sizes[0], sizes[1]))
-            total += sizes[0] + sizes[1]
+            blocks, c0 = [], 0
+            for cb in (split if split is not None else (cin,)):
+                sizes = [lib.vae2_conv2d_packed_size(cout, cb, k, mode) for mode in (0, 1)]
+                blocks.append((c0, cb, total, sizes[0], total + sizes[0], sizes[1]))
+                total += sizes[0] + sizes[1]
+                c0 += cb
+            if c0 != cin:
+                raise ValueError(f"column split {split} does not cover {cin} input channels")
+            self._blocks.append(blocks)
         self.buf = torch.empty((total,), dtype=_F32,
                                device=self.weights[0].device if self.weights else None)
-        self._views = [(self.buf[a:a + na], self.buf[b:b + nb]) for a, na, b, nb in layout]
+        self._views = [[(self.buf[a:a + na], self.buf[b:b + nb]) for _, _, a, na, b, nb in bl]
+                       for bl in self._blocks]
         self._build_jobs()
         self.run()
 
@@ -173,13 +185,16 @@ class PackPlan:
             self.njobs = 0
             return
         self._ptrs = [w.data_ptr() for w in self.weights]
-        jobs = (_lib.PackJob * (2 * len(self.weights)))()
-        for i, (w, views) in enumerate(zip(self.weights, self._views)):
+        jobs = []
+        for w, split, blocks, views in zip(self.weights, self.splits, self._blocks, self._views):
             cout, cin, k, _ = w.shape
-            for mode in (0, 1):
-                jobs[2 * i + mode] = _lib.PackJob(w.data_ptr(), views[mode].data_ptr(),
-                                                  cout, cin, k, mode)
-        host = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8)
+            ld = cin * k * k if split is not None else 0
+            for (c0, cb, *_), vv in zip(blocks, views):
+                for mode in (0, 1):
+                    jobs.append(_lib.PackJob(w.data_ptr() + 4 * c0 * k * k, vv[mode].data_ptr(),
+                                             cout, cb, k, mode, ld, 0))
+        arr = (_lib.PackJob * len(jobs))(*jobs)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self.jobs = host.to(self.buf.device)
         self.njobs = len(jobs)
 
@@ -190,8 +205,11 @@ class PackPlan:
         if any(w.data_ptr() != p for w, p in zip(self.weights, self._ptrs)):
             self._build_jobs()
         call("vae2_conv2d_pack_weights", ptr(self.jobs), self.njobs, stream_ptr())
-        for w, views in zip(self.weights, self._views):
-            w._vae2_packed = (views[0], views[1], w._version, w.data_ptr())
+        for w, split, views in zip(self.weights, self.splits, self._views):
+            if split is None:
+                w._vae2_packed = (views[0][0], views[0][1], w._version, w.data_ptr())
+            else:
+                w._vae2_packed_cols = (tuple(split), views, w._version, w.data_ptr())
 
     def bump_versions(self):
         """Mark the weights modified (an in-place kernel wrote them) and re-pack."""
@@ -208,6 +226,22 @@ def packed_weight(weight, mode):
     out = torch.empty((_lib.load().vae2_conv2d_packed_size(cout, cin, k, mode),),
                       dtype=_F32, device=weight.device)
     call("vae2_conv2d_pack_weight", ptr(weight), cout, cin, k, mode, ptr(out), stream_ptr())
+    return out
+
+
+def packed_weight_cols(weight, split, j, mode):
+    """Packed layout of input-channel block j of `weight` under the column split."""
+    split = tuple(split)
+    cached = getattr(weight, "_vae2_packed_cols", None)
+    if (cached is not None and cached[0] == split and cached[2] == weight._version and
+            cached[3] == weight.data_ptr()):
+        return cached[1][j][mode]
+    cout, cin, k, _ = weight.shape
+    c0, cb = sum(split[:j]), split[j]
+    out = torch.empty((_lib.load().vae2_conv2d_packed_size(cout, cb, k, mode),),
+                      dtype=_F32, device=weight.device)
+    call("vae2_conv2d_pack_weight_ld", ctypes.c_void_p(weight.data_ptr() + 4 * c0 * k * k),
+         cout, cb, k, mode, cin * k * k, ptr(out), stream_ptr())
     return out
 
 
