@@ -198,12 +198,15 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
  * upsampling, so with W = [W0 | W1 | W2 | W3] split by input block
  *     y = W0 x0 + bias + up(W1 x1) + up(W2 x2) + up(W3 x3),
  * the z_s = W_s x_s computed at their own resolution (vae2_conv2d_fwd).  This call:
- * y = conv1x1(x, w) + bias + sum_s bilinear_up(ups[s]) to y's h, w (align_corners=False;
- * channels [0, yd->c) of each ups[s], nup <= 3), w = the [Cout][Cin0] block of a 1x1
- * weight with rows w_ld floats apart (Cin0 <= 32); optional BN partial statistics
- * stats [2][vae2_conv1x1_upsum_stats_rows(yd)][Cout].                              */
+ * y = conv1x1(x, wp) + bias + sum_s bilinear_up(ups[s]) to y's h, w (align_corners=False;
+ * channels [0, yd->c) of each ups[s], nup <= 3), wp = the W0 block packed as
+ * vae2_conv2d_pack_weight(_ld) mode 0 (Cin0 <= 32); optional BN partial statistics
+ * stats [2][vae2_conv1x1_upsum_stats_rows(yd)][Cout].
+ * y is written in the 64-channel-blocked layout B64 (not NHWC):
+ *     element (p, c) at y[(c / 64) * P * 64 + p * 64 + c % 64],  P = n*h*w,
+ * i.e. ceil(Cout/64) * P * 64 floats (yd->ps is ignored).                          */
 int64_t vae2_conv1x1_upsum_stats_rows(const vae2_act* yd);
-int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, int64_t w_ld,
+int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
                            const float* bias, int nup, const float* const* ups,
                            const vae2_act* upds, float* y, const vae2_act* yd, float* stats,
                            void* stream);
@@ -212,7 +215,7 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, i
  * :839-847, :897-905, :955-963): BatchNorm (coefficients `save` [4][C] from
  * vae2_bn_reduce_finalize / _finalize) -> ReLU -> Conv1x1(C -> cout2 <= 4, bias),
  * reading the pre-BN conv output y once per pass; the ReLU output is never stored.
- * y: 16-byte aligned NHWC, ps % 4 == 0, C <= 1024.  w2 = [cout2][C] (the conv weight
+ * y: the B64 layout of vae2_conv1x1_upsum_fwd, 16-byte aligned, C <= 1024 (dy: NHWC).  w2 = [cout2][C] (the conv weight
  * [cout2][C][1][1]), b2 = [cout2] or NULL.
  *   out[p][o] = b2[o] + sum_c w2[o][c] * relu(y[p][c]*scale[c] + shift[c])        */
 int vae2_head_out_fwd(const float* y, const vae2_act* yd, const float* save, const float* w2,

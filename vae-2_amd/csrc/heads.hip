@@ -23,6 +23,14 @@ constexpr int kHeadMaxOut = 4;
 
 __device__ __forceinline__ f4 hld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
+// The wide conv's output y lives in a 64-channel-blocked layout ("B64"):
+//   element (p, c) at y[(c / 64) * P * 64 + p * 64 + c % 64],  P = N*H*W pixels,
+// so a workgroup producing a 64-channel block of a pixel run writes one contiguous
+// region (NHWC rows of C = 270 would be written in partial 128-byte lines).
+__device__ __forceinline__ const float* yb_at(const float* y, int64_t P, int64_t p, int c) {
+  return y + (int64_t)(c >> 6) * P * 64 + p * 64 + (c & 63);
+}
+
 __device__ __forceinline__ f4 hchan4(const float* a, int c, int C) {
   f4 v;
 #pragma unroll
@@ -55,9 +63,8 @@ __global__ __launch_bounds__(256) void head_out_fwd_kernel(
     float acc[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) acc[o] = 0.f;
-    const float* yp = y + p * yd.ps;
     for (int q = l; q < c4; q += 16) {
-      const f4 v = hld4(yp + 4 * q);
+      const f4 v = hld4(yb_at(y, P, p, 4 * q));
       const f4 a = ssc[q], b = ssh[q];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
 #pragma unroll
     for (int o = 0; o < CO; ++o) { dw[o] = s0; db[o] = 0.f; }
     for (int64_t p = p0 + r; p < p1; p += rows) {
-      const f4 v = hld4(y + p * yd.ps + c);
+      const f4 v = hld4(yb_at(y, P, p, c));
       float d[CO];
 #pragma unroll
       for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
@@ -223,7 +230,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
     }
     f4 sdy = {0.f, 0.f, 0.f, 0.f};
     for (int64_t p = p0 + r; p < p1; p += rows) {
-      const f4 v = hld4(y + p * yd.ps + c);
+      const f4 v = hld4(yb_at(y, P, p, c));
       float d[CO];
 #pragma unroll
       for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
@@ -261,30 +268,30 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
 }
 
 // ------------------------------------------------------------------ up-sum ----
-// y[n,oy,x,c] = sum_k x0[n,oy,x,k] w[c][k] + sum_s up(z_s)[n,oy,x,c] + bias[c]
+// y[n,oy,x,c] = sum_k x0[n,oy,x,k] W0[c][k] + sum_s up(z_s)[n,oy,x,c] + bias[c]
 // (the wide head conv split by branch; z_s = W_s y_s at the branch resolution).
-// Workgroup = (image row, 64-pixel chunk, 64-channel block), lane = channel, W0 column
-// in registers.  Staged in LDS once per workgroup: the chunk's x0 pixels (16-byte
-// rows), each source's two contributing rows blended vertically over the chunk's
-// source-column window, and per-pixel horizontal interpolation tables; every output
-// pixel then costs ceil(cin/4) + 3 broadcast reads, 2 reads per source and cin + 2*nup
-// FMAs.  Coalesced 256-byte NHWC segments in and out; BN partial sums per (row, chunk).
-constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32;
+// Workgroup = (image row, 64-pixel chunk, 64-channel block); wave w owns pixels
+// 16w..16w+15.  The full-resolution block W0 x0 (K = Cin0 <= 32) is a 16x64 MFMA tile
+// per wave (v_mfma_f32_16x16x4f32, packed W0, fragments straight from global/L2).  Each
+// source's two contributing rows are blended vertically once into LDS (batched loads,
+// one memory round trip) with per-pixel horizontal tables; the epilogue adds the two
+// horizontal taps per source, the bias, writes y and the BN partial sums.
+constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32, kUsVS = 68;  // VS: LDS column stride
 
 struct UpSum {
   const float* x;
   int x_ps, cin, cin4, H, W;
-  const float* w;
-  int w_ld;
+  const float* wp;  // packed [round_up(C,64)][cin4]
   const float* bias;
   const float* z[3];
   int zh[3], zw[3], zps[3];
   float sh[3], sw[3];
-  int vcols;
+  int vcols[3];  // staged source columns per 64-pixel chunk
   float* y;
   int y_ps, C;
   float* stats;  // [2][rows][C], row = (n*H + oy)*nxb + xb
   int rows, nxb;
+  int dbg;
 };
 
 template <int NUP>
@@ -292,84 +299,140 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   extern __shared__ __attribute__((aligned(16))) float usm[];
   __shared__ float red[2][4][kUsCB];
   f4* tab = reinterpret_cast<f4*>(usm);                  // [NUP][kUsXB] {i0, i1, l0, l1}
-  float* xs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [kUsXB][cin4]
-  float* vs = xs + kUsXB * p.cin4;                        // [NUP][vcols][64]
+  float* vs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [sum_s vcols_s][kUsVS]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = blockIdx.x;
+  const int g = lane >> 4, r = lane & 15;
+  // block order: chunk fastest, then channel block, then image row, so the workgroups
+  // in flight cover a few consecutive rows (page / L2 locality of the NHWC rows)
+  const int ncb = (p.C + kUsCB - 1) / kUsCB;
+  const int xb = blockIdx.x % p.nxb, x0 = xb * kUsXB;
+  const int cbi = (blockIdx.x / p.nxb) % ncb;
+  const int row = blockIdx.x / (p.nxb * ncb);
   const int n = row / p.H, oy = row - n * p.H;
-  const int xb = blockIdx.y, x0 = xb * kUsXB;
-  const int c = blockIdx.z * kUsCB + lane;
-  const bool cok = c < p.C;
+  const int c0 = cbi * kUsCB;
   const int xn = p.W - x0 < kUsXB ? p.W - x0 : kUsXB;
-  float wreg[kUsMaxCin];
-#pragma unroll
-  for (int k = 0; k < kUsMaxCin; ++k)
-    wreg[k] = (k < p.cin && cok) ? p.w[(int64_t)c * p.w_ld + k] : 0.f;
+  // ---- MFMA operands (issued first: their latency overlaps the staging below) ----
+  const int kq = p.cin4 >> 2;
   const float* xrow = p.x + ((int64_t)row * p.W + x0) * p.x_ps;
-  for (int i = threadIdx.x; i < xn * p.cin4; i += 256) {
-    const int px = i / p.cin4, k = i - px * p.cin4;
-    xs[i] = k < p.cin ? xrow[(int64_t)px * p.x_ps + k] : 0.f;
+  const int pxa = 16 * wave + r;
+  float fa[kUsMaxCin / 4], fb[kUsMaxCin / 4][4];
+#pragma unroll
+  for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+    const int k = 4 * kb + g;
+    fa[kb] = (!(p.dbg & 1) && kb < kq && pxa < xn && k < p.cin) ? xrow[(int64_t)pxa * p.x_ps + k] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fb[kb][j] = (!(p.dbg & 1) && kb < kq) ? p.wp[(int64_t)(c0 + 16 * j + r) * p.cin4 + k] : 0.f;
   }
-  int vlo[3] = {0, 0, 0};
+  // ---- vertical blends of each source over the chunk's source-column window ----
+  constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
+  const int c = c0 + lane;
+  const bool cok = c < p.C;
+  float a0[NUP > 0 ? NUP : 1][VU], a1[NUP > 0 ? NUP : 1][VU];
+  int vlo[3] = {0, 0, 0}, vhi[3] = {0, 0, 0}, voff[3] = {0, 0, 0};
+  Lerp ly[3];
 #pragma unroll
   for (int s = 0; s < NUP; ++s) {
     vlo[s] = lerp_index(x0, p.zw[s], p.sw[s]).i0;
-    const int hi = lerp_index(x0 + xn - 1, p.zw[s], p.sw[s]).i1;
+    vhi[s] = lerp_index(x0 + xn - 1, p.zw[s], p.sw[s]).i1;
+    voff[s] = s == 0 ? 0 : voff[s - 1] + p.vcols[s - 1];
+    ly[s] = lerp_index(oy, p.zh[s], p.sh[s]);
+    const int64_t ibase = (int64_t)n * p.zh[s];
+    const float* r0 = p.z[s] + (ibase + ly[s].i0) * p.zw[s] * p.zps[s] + c;
+    const float* r1 = p.z[s] + (ibase + ly[s].i1) * p.zw[s] * p.zps[s] + c;
+#pragma unroll
+    for (int u = 0; u < VU; ++u) {
+      const int ix = vlo[s] + wave + 4 * u;
+      const bool ok = !(p.dbg & 2) && cok && ix <= vhi[s];
+      a0[s][u] = ok ? r0[(int64_t)ix * p.zps[s]] : 0.f;
+      a1[s][u] = ok ? r1[(int64_t)ix * p.zps[s]] : 0.f;
+    }
     if (threadIdx.x < xn) {
       const Lerp lx = lerp_index(x0 + threadIdx.x, p.zw[s], p.sw[s]);
       tab[s * kUsXB + threadIdx.x] =
-          f4{__int_as_float(lx.i0 - vlo[s]), __int_as_float(lx.i1 - vlo[s]), lx.l0, lx.l1};
+          f4{__int_as_float((voff[s] + lx.i0 - vlo[s]) * kUsVS),
+             __int_as_float((voff[s] + lx.i1 - vlo[s]) * kUsVS), lx.l0, lx.l1};
     }
-    const Lerp ly = lerp_index(oy, p.zh[s], p.sh[s]);
-    const int64_t ibase = (int64_t)n * p.zh[s];
-    const float* r0 = p.z[s] + (ibase + ly.i0) * p.zw[s] * p.zps[s] + c;
-    const float* r1 = p.z[s] + (ibase + ly.i1) * p.zw[s] * p.zps[s] + c;
-    for (int ix = vlo[s] + wave; ix <= hi; ix += 4) {
-      float v = 0.f;
-      if (cok) v = ly.l0 * r0[(int64_t)ix * p.zps[s]] + ly.l1 * r1[(int64_t)ix * p.zps[s]];
-      vs[(s * p.vcols + (ix - vlo[s])) * kUsCB + lane] = v;
+  }
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+#pragma unroll
+    for (int u = 0; u < VU; ++u) {
+      const int ix = vlo[s] + wave + 4 * u;
+      if (ix <= vhi[s])
+        vs[(voff[s] + ix - vlo[s]) * kUsVS + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
+    }
+  }
+  // ---- W0 x0: acc[j][e] = pixel 16*wave + 4g + e, channel c0 + 16j + r ----
+  f4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+    if (kb < kq) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kb], fb[kb][j], acc[j], 0, 0, 0);
     }
   }
   __syncthreads();
-  float s1 = 0.f, s2 = 0.f;
-  const float b = (p.bias && cok) ? p.bias[c] : 0.f;
-  float* yout = p.y + ((int64_t)row * p.W + x0) * p.y_ps + c;
-  for (int px = wave; px < xn; px += 4) {
-    float acc = 0.f;
-    const f4* xq = reinterpret_cast<const f4*>(xs + px * p.cin4);
+  // ---- epilogue ----
+  float bj[4], s1[4], s2[4];
 #pragma unroll
-    for (int q = 0; q < kUsMaxCin / 4; ++q) {
-      if (4 * q < p.cin) {
-        const f4 xv = xq[q];
-        acc = __builtin_fmaf(xv[0], wreg[4 * q], acc);
-        acc = __builtin_fmaf(xv[1], wreg[4 * q + 1], acc);
-        acc = __builtin_fmaf(xv[2], wreg[4 * q + 2], acc);
-        acc = __builtin_fmaf(xv[3], wreg[4 * q + 3], acc);
+  for (int j = 0; j < 4; ++j) {
+    const int cj = c0 + 16 * j + r;
+    bj[j] = (p.bias && cj < p.C) ? p.bias[cj] : 0.f;
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+  const int64_t P = (int64_t)(p.rows / p.nxb) * p.W;
+  float* ybase = p.y + (int64_t)cbi * P * 64 + ((int64_t)row * p.W + x0) * 64 + r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int px = 16 * wave + 4 * g + e;
+    if (px >= xn) continue;
+    f4 t[3];
+#pragma unroll
+    for (int s = 0; s < NUP; ++s) t[s] = tab[s * kUsXB + px];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[j][e];
+#pragma unroll
+      for (int s = 0; s < NUP; ++s) {
+        if (p.dbg & 4) break;
+        const float* vj = vs + 16 * j + r;
+        v += t[s][2] * vj[__float_as_int(t[s][0])] + t[s][3] * vj[__float_as_int(t[s][1])];
       }
-    }
-#pragma unroll
-    for (int s = 0; s < NUP; ++s) {
-      const f4 t = tab[s * kUsXB + px];
-      const float* v = vs + s * p.vcols * kUsCB + lane;
-      acc += t[2] * v[__float_as_int(t[0]) * kUsCB] + t[3] * v[__float_as_int(t[1]) * kUsCB];
-    }
-    const float o = acc + b;
-    if (cok) {
-      yout[(int64_t)px * p.y_ps] = o;
-      s1 += o;
-      s2 += o * o;
+      v += bj[j];
+      if (c0 + 16 * j + r < p.C) {
+        ybase[(int64_t)px * 64 + 16 * j] = v;
+        s1[j] += v;
+        s2[j] += v * v;
+      }
     }
   }
   if (p.stats) {
-    red[0][wave][lane] = s1;
-    red[1][wave][lane] = s2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[0][wave][16 * j + r] = s1[j];
+        red[1][wave][16 * j + r] = s2[j];
+      }
+    }
     __syncthreads();
     if (wave == 0 && cok) {
-      const int r = row * p.nxb + xb;
-      p.stats[(int64_t)r * p.C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] +
-                                      red[0][3][lane];
-      p.stats[((int64_t)p.rows + r) * p.C + c] = red[1][0][lane] + red[1][1][lane] +
-                                                 red[1][2][lane] + red[1][3][lane];
+      const int rr = row * p.nxb + xb;
+      p.stats[(int64_t)rr * p.C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] +
+                                       red[0][3][lane];
+      p.stats[((int64_t)p.rows + rr) * p.C + c] = red[1][0][lane] + red[1][1][lane] +
+                                                  red[1][2][lane] + red[1][3][lane];
     }
   }
 }
@@ -415,10 +478,10 @@ template <int NUP>
 __global__ __launch_bounds__(256) void up_adj_h_kernel(UpAdj p) {
   extern __shared__ __attribute__((aligned(16))) float asm_[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = blockIdx.x;  // n*H + oy
-  const int xb = blockIdx.y;
-  const int c = blockIdx.z * 64 + lane;
-  const bool cok = c < p.C;
+  const int ncb = (p.C + 63) / 64;
+  const int xb = blockIdx.x % p.nxb;
+  const int cbi = (blockIdx.x / p.nxb) % ncb;
+  const int row = blockIdx.x / (p.nxb * ncb);  // n*H + oy
   const int span = kUsXB + 2 * p.halo;
   f4* tab = reinterpret_cast<f4*>(asm_);              // [NUP][span]
   float* st = asm_ + 4 * NUP * span;                  // [span][64]
@@ -437,8 +500,6 @@ __global__ __launch_bounds__(256) void up_adj_h_kernel(UpAdj p) {
   }
   if (whi < wlo) return;  // no owned columns (uniform over the workgroup)
   const int cnt = whi - wlo + 1;  // <= span (host-sized halo)
-  const float* drow = p.dy + (int64_t)row * p.W * p.dy_ps + c;
-  for (int i = wave; i < cnt; i += 4) st[i * 64 + lane] = cok ? drow[(int64_t)(wlo + i) * p.dy_ps] : 0.f;
 #pragma unroll
   for (int s = 0; s < NUP; ++s) {
     for (int i = threadIdx.x; i < cnt; i += 256) {
@@ -446,22 +507,65 @@ __global__ __launch_bounds__(256) void up_adj_h_kernel(UpAdj p) {
       tab[s * span + i] = f4{__int_as_float(lx.i0), __int_as_float(lx.i1), lx.l0, lx.l1};
     }
   }
-  __syncthreads();
-  if (!cok) return;
+  {
+    const int c = cbi * 64 + lane;
+    const bool cok = c < p.C;
+    const float* drow = p.dy + (int64_t)row * p.W * p.dy_ps + c;
+    {
+      constexpr int SU = 24;  // pixels per wave in flight (span <= 96: one round trip)
+      for (int i0 = wave; i0 < cnt; i0 += 4 * SU) {
+        float v[SU];
 #pragma unroll
-  for (int s = 0; s < NUP; ++s) {
-    float* hrow = p.hb[s] + (int64_t)row * p.zw[s] * p.C + c;
-    for (int ix = ib[s] + wave; ix < ie[s]; ix += 4) {
-      int lo, hi;
-      adj_window(ix, p.zw[s], p.W, p.sw[s], lo, hi);
-      float acc = 0.f;
-      for (int ox = lo; ox <= hi; ++ox) {
-        const f4 t = tab[s * span + (ox - wlo)];
-        const float w = (__float_as_int(t[0]) == ix ? t[2] : 0.f) +
-                        (__float_as_int(t[1]) == ix ? t[3] : 0.f);
-        acc = __builtin_fmaf(w, st[(ox - wlo) * 64 + lane], acc);
+        for (int u = 0; u < SU; ++u) {
+          const int i = i0 + 4 * u;
+          v[u] = (cok && i < cnt) ? drow[(int64_t)(wlo + i) * p.dy_ps] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int i = i0 + 4 * u;
+          if (i < cnt) st[i * 64 + lane] = v[u];
+        }
       }
-      hrow[(int64_t)ix * p.C] = acc;
+    }
+    __syncthreads();
+    if (!cok) return;
+    // Work items: (source, half of its owned columns); wave w streams items w, w+4, ...
+    // Streaming: pixels ox ascend, so each ox adds l0 to column i0 and l1 to i1 in
+    // {i0, i0+1} with i0 non-decreasing; two running sums (columns cur, cur+1) are kept
+    // and column cur is final (stored) once i0 moves past it.
+    for (int item = wave; item < 2 * NUP; item += 4) {
+      const int s = item % NUP, half = item / NUP;
+      const int mid = ib[s] + (ie[s] - ib[s] + 1) / 2;
+      const int cb = half ? mid : ib[s], ce = half ? ie[s] : mid;
+      if (cb >= ce) continue;
+      int lo, hi, lo2, hi2;
+      adj_window(cb, p.zw[s], p.W, p.sw[s], lo, hi);
+      adj_window(ce - 1, p.zw[s], p.W, p.sw[s], lo2, hi2);
+      float* hrow = p.hb[s] + (int64_t)row * p.zw[s] * p.C + c;
+      const f4* ts = tab + s * span - wlo;
+      const float* sv = st - wlo * 64 + lane;
+      int cur = cb - 1;
+      float a0 = 0.f, a1 = 0.f;  // sums of columns cur, cur + 1
+      for (int ox = lo; ox <= hi2; ++ox) {
+        const f4 t = ts[ox];  // wave-uniform: moved to scalar registers
+        const int i0 = __builtin_amdgcn_readfirstlane(__float_as_int(t[0]));
+        const int i1 = __builtin_amdgcn_readfirstlane(__float_as_int(t[1]));
+        const float l0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t[2])));
+        const float l1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t[3])));
+        const float v = sv[ox * 64];
+        while (cur < i0) {  // wave-uniform
+          if (cur >= cb && cur < ce) hrow[(int64_t)cur * p.C] = a0;
+          a0 = a1;
+          a1 = 0.f;
+          ++cur;
+        }
+        // now i0 <= cur (i0 < cur only left of the owned range: not ours)
+        if (i0 == cur) a0 = __builtin_fmaf(l0, v, a0);
+        if (i1 == cur) a0 = __builtin_fmaf(l1, v, a0);
+        else if (i1 == cur + 1) a1 = __builtin_fmaf(l1, v, a1);
+      }
+      if (cur >= cb && cur < ce) hrow[(int64_t)cur * p.C] = a0;
+      if (cur + 1 >= cb && cur + 1 < ce) hrow[(int64_t)(cur + 1) * p.C] = a1;
     }
   }
 }
@@ -484,10 +588,18 @@ __global__ __launch_bounds__(256) void up_adj_v_kernel(UpAdj p, int s) {
   const float* hb = p.hb[s] + ((int64_t)n * p.H + lo) * p.zw[s] * p.C + c;
   float* out = p.dx[s] + (int64_t)row * p.zw[s] * p.dx_ps[s] + c;
   const int64_t rs = (int64_t)p.zw[s] * p.C;
-  for (int ix = wave; ix < p.zw[s]; ix += 4) {
-    float acc = 0.f;
-    for (int t = 0; t < cnt; ++t) acc = __builtin_fmaf(wy[t], hb[t * rs + (int64_t)ix * p.C], acc);
-    out[(int64_t)ix * p.dx_ps[s]] = acc;
+  for (int ix = wave; ix < p.zw[s]; ix += 8) {
+    const bool two = ix + 4 < p.zw[s];
+    const float* h0 = hb + (int64_t)ix * p.C;
+    const float* h1 = hb + (int64_t)(two ? ix + 4 : ix) * p.C;
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 4
+    for (int t = 0; t < cnt; ++t) {
+      acc0 = __builtin_fmaf(wy[t], h0[t * rs], acc0);
+      acc1 = __builtin_fmaf(wy[t], h1[t * rs], acc1);
+    }
+    out[(int64_t)ix * p.dx_ps[s]] = acc0;
+    if (two) out[(int64_t)(ix + 4) * p.dx_ps[s]] = acc1;
   }
 }
 
@@ -498,8 +610,8 @@ static int64_t head_ppb(int64_t P) {
 }
 
 static bool head_args_ok(const float* y, const vae2_act* yd, int cout2) {
-  return y && act_ok(yd) && ((uintptr_t)y % 16 == 0) && yd->ps % 4 == 0 &&
-         (yd->c + 3) / 4 <= 256 && cout2 >= 1 && cout2 <= kHeadMaxOut;
+  return y && act_ok(yd) && ((uintptr_t)y % 16 == 0) && (yd->c + 3) / 4 <= 256 &&
+         cout2 >= 1 && cout2 <= kHeadMaxOut;
 }
 
 #define HEAD_DISPATCH(CO_, KERNEL, ...)                                   \
@@ -598,20 +710,20 @@ int64_t vae2_conv1x1_upsum_stats_rows(const vae2_act* yd) {
   return yd->n * yd->h * ceil_div(yd->w, kUsXB);
 }
 
-int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, int64_t w_ld,
+int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
                            const float* bias, int nup, const float* const* ups,
                            const vae2_act* upds, float* y, const vae2_act* yd, float* stats,
                            void* stream) {
   const char* fn = "vae2_conv1x1_upsum_fwd";
-  VAE2_REQUIRE(x && w && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(x && wp && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
   VAE2_REQUIRE(xd->n == yd->n && xd->h == yd->h && xd->w == yd->w, fn, "x / y shape mismatch");
-  VAE2_REQUIRE(w_ld >= xd->c && xd->c <= kUsMaxCin, fn, "bad weight block (Cin0 <= 32)");
+  VAE2_REQUIRE(xd->c <= kUsMaxCin, fn, "Cin0 > 32");
   VAE2_REQUIRE(nup >= 0 && nup <= 3 && (nup == 0 || (ups && upds)), fn, "bad up-sum terms");
   UpSum p{};
   p.x = x; p.x_ps = (int)xd->ps; p.cin = (int)xd->c; p.cin4 = ((int)xd->c + 3) / 4 * 4;
   p.H = (int)yd->h; p.W = (int)yd->w;
-  p.w = w; p.w_ld = (int)w_ld; p.bias = bias;
-  int vcols = 1;
+  p.wp = wp; p.bias = bias;
+  int vtot = 0;
   for (int s = 0; s < nup; ++s) {
     const vae2_act* u = &upds[s];
     VAE2_REQUIRE(ups[s] && act_ok(u) && u->n == yd->n && u->c >= yd->c && u->h <= yd->h &&
@@ -619,18 +731,22 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* w, i
     p.z[s] = ups[s]; p.zh[s] = (int)u->h; p.zw[s] = (int)u->w; p.zps[s] = (int)u->ps;
     p.sh[s] = (float)u->h / (float)yd->h;
     p.sw[s] = (float)u->w / (float)yd->w;
-    const int vc = (int)ceilf(p.sw[s] * kUsXB) + 3;
-    if (vc > vcols) vcols = vc;
+    p.vcols[s] = (int)ceilf(p.sw[s] * kUsXB) + 3;
+    VAE2_REQUIRE(p.vcols[s] <= 48, fn, "source wider than half the output (upsampling only)");
+    vtot += p.vcols[s];
   }
-  p.vcols = vcols;
   p.y = y; p.y_ps = (int)yd->ps; p.C = (int)yd->c;
   p.stats = stats;
   p.nxb = (int)ceil_div(yd->w, kUsXB);
   p.rows = (int)vae2_conv1x1_upsum_stats_rows(yd);
+  {
+    const char* e = getenv("VAE2_UPSUM_DEBUG");
+    p.dbg = e ? atoi(e) : 0;
+  }
   const int nu = nup > 0 ? nup : 1;
-  const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)kUsXB * p.cin4 +
-                      (size_t)nu * vcols * kUsCB) * sizeof(float);
-  dim3 grid((unsigned)(yd->n * yd->h), (unsigned)p.nxb, (unsigned)ceil_div(yd->c, kUsCB));
+  const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1) * kUsVS) *
+                     sizeof(float);
+  dim3 grid((unsigned)(yd->n * yd->h * p.nxb * ceil_div(yd->c, kUsCB)));
   hipStream_t st = as_stream(stream);
   switch (nup) {
     case 0: hipLaunchKernelGGL(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
@@ -681,7 +797,7 @@ int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n
   const int span = kUsXB + 2 * p.halo;
   const size_t shm = (size_t)(4 * n + 64) * span * sizeof(float);
   VAE2_REQUIRE(shm <= 64 * 1024, fn, "upsampling ratio too large for the LDS tile");
-  dim3 grid((unsigned)(dyd->n * dyd->h), (unsigned)p.nxb, cb);
+  dim3 grid((unsigned)(dyd->n * dyd->h * p.nxb * cb));
   hipStream_t st = as_stream(stream);
   switch (n) {
     case 1: hipLaunchKernelGGL(up_adj_h_kernel<1>, grid, dim3(256), shm, st, p); break;

@@ -49,8 +49,8 @@ _SIGS = {
     "vae2_conv2d_bwd_weight_ld": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_i64, c_vp, c_int,
                                           c_int, c_int, c_int, c_vp, c_i64, c_vp]),
     "vae2_conv1x1_upsum_stats_rows": (c_i64, [P_ACT]),
-    "vae2_conv1x1_upsum_fwd": (c_int, [c_vp, P_ACT, c_vp, c_i64, c_vp, c_int, ctypes.POINTER(c_vp),
-                                       P_ACT, c_vp, P_ACT, c_vp, c_vp]),
+    "vae2_conv1x1_upsum_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_int, ctypes.POINTER(c_vp), P_ACT,
+                                       c_vp, P_ACT, c_vp, c_vp]),
     "vae2_upsample_bilinear_bwd_multi_ws_size": (c_i64, [P_ACT, c_int, P_ACT]),
     "vae2_upsample_bilinear_bwd_multi": (c_int, [c_vp, P_ACT, c_int, ctypes.POINTER(c_vp), P_ACT,
                                                  c_vp, c_i64, c_vp]),

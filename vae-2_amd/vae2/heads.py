@@ -99,11 +99,12 @@ class _Heads(torch.autograd.Function):
                 zs.append((z, zp, za))
             ups = (ctypes.c_void_p * 3)(*[zp for _, zp, _ in zs])
             upds = (Act * 3)(*[za for _, _, za in zs])
-            y = new_act((n, H, W, C), x0)
-            yp, ya = act_of(y)
+            y = _empty((-(-C // 64) * n * H * W * 64,), x0)  # B64 layout (heads.hip)
+            yp, ya = ptr(y), yshape
             stats = _empty((2 * rows * C,), x0) if training[k] else None
-            call("vae2_conv1x1_upsum_fwd", x0p, ctypes.byref(x0a), ptr(w), C, ptr(b), nb - 1,
-                 ups, upds, yp, ctypes.byref(ya), ptr(stats), s)
+            call("vae2_conv1x1_upsum_fwd", x0p, ctypes.byref(x0a),
+                 ptr(packed_weight_cols(w, split, 0, 0)), ptr(b), nb - 1, ups, upds, yp,
+                 ctypes.byref(ya), ptr(stats), s)
             save = _empty((4 * C,), x0)
             if training[k]:
                 sums = _empty((2 * C,), x0, torch.float64)
@@ -164,7 +165,7 @@ class _Heads(torch.autograd.Function):
         for k in range(nh):
             w, b, gamma, beta, w2, b2 = ctx.params[_PER_HEAD * k:_PER_HEAD * (k + 1)]
             y, save = yv[k], saves[k]
-            yp, ya = act_of(y)
+            yp, ya = ptr(y), Act(*ys[0].shape[:3], C, C)
             dk = dout[..., ncls * k:ncls * (k + 1)]
             dkp, dka = act_of(dk)
             wsz = lib.vae2_head_out_bwd_ws_size(ctypes.byref(ya), ncls)
@@ -178,7 +179,7 @@ class _Heads(torch.autograd.Function):
                  ctypes.byref(dka), ptr(lsums), ptr(gsink), ptr(btsink), ptr(w2sink),
                  ptr(b2sink), ptr(ws), wsz, s)
             gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
-            dy = new_act(tuple(y.shape), y)
+            dy = new_act((*ys[0].shape[:3], C), y)
             dyp, dya = act_of(dy)
             bsink, bret = _grad_sink(b)
             call("vae2_head_out_bwd_apply", yp, ctypes.byref(ya), ptr(save), ptr(gamma), ptr(w2),
