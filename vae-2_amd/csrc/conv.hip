@@ -126,10 +126,23 @@ struct IGemm {
   float beta;
   float* stats;  // [2][gridDim.x][n] or null
   FastDiv hw_div, w_div;  // divide by g_h*g_w, g_w
+  // Strided data gradient: one launch covers every stride-parity class of the input
+  // pixels, class = blockIdx.z (gridDim.z == 1: the fields above are used as they are).
+  struct Cls {
+    int g_h, g_w, nth, ntw, dh0, dw0, kh0, kw0, y_offh, y_offw;
+    FastDiv hw_div, w_div;
+  } cls[4];
 };
 
 template <int TM, int TN, bool VEC, int ROLE>
-__global__ __launch_bounds__(256) void igemm_kernel(IGemm p) {
+__global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
+  IGemm p = pin;
+  if (gridDim.z > 1) {
+    const IGemm::Cls& c = pin.cls[blockIdx.z];
+    p.g_h = c.g_h; p.g_w = c.g_w; p.nth = c.nth; p.ntw = c.ntw;
+    p.dh0 = c.dh0; p.dw0 = c.dw0; p.kh0 = c.kh0; p.kw0 = c.kw0;
+    p.y_offh = c.y_offh; p.y_offw = c.y_offw; p.hw_div = c.hw_div; p.w_div = c.w_div;
+  }
   constexpr int BN = 16 * TN;
   __shared__ float red[4][2][BN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -544,13 +557,24 @@ static bool vec_ok(const float* a, int ps) {
   return ((uintptr_t)a % 16 == 0) && (ps % 4 == 0);
 }
 
-static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn) {
+// ncls > 1: p.cls[0..ncls) hold the parity classes; the grid covers the largest one.
+static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls = 1) {
   int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
+  if (ncls > 1) {
+    M = 0;
+    for (int c = 0; c < ncls; ++c) {
+      IGemm::Cls& k = p.cls[c];
+      k.hw_div = FastDiv((uint32_t)(k.g_h * k.g_w));
+      k.w_div = FastDiv((uint32_t)k.g_w);
+      const int64_t mc = (int64_t)p.g_n * k.g_h * k.g_w;
+      if (mc > M) M = mc;
+    }
+  }
   if (M == 0) return 0;
   Tile t = pick_tile(M, p.n, wide_ok(M, p.n, p.nth * p.ntw));
   p.hw_div = FastDiv((uint32_t)(p.g_h * p.g_w));
   p.w_div = FastDiv((uint32_t)p.g_w);
-  dim3 grid((unsigned)ceil_div(M, 64 * t.tm), (unsigned)t.nblk);
+  dim3 grid((unsigned)ceil_div(M, 64 * t.tm), (unsigned)t.nblk, (unsigned)ncls);
   bool vec = vec_ok(p.a, p.a_ps);
   if (role == 0) {
     if (vec) launch_tm<true, 0>(p, t, grid, s);
@@ -623,8 +647,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int ohw = p.o_h * p.o_w;
-  for (int pc = pbeg + 16 * wave; pc < pend; pc += 64) {
-    f4 fa[TM], fb[TN];
+  // chunk loads (pixels past pend load 0), double-buffered in registers: the next
+  // chunk's loads are in flight across this chunk's MFMAs
+  auto load = [&](int pc, f4* fa, f4* fb) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int pix = pc + 4 * g + s;
@@ -648,6 +673,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
         fb[j][s] = load1(xr, ok ? (uint32_t)(xc + boff[j]) * 4u : kOOB);
       }
     }
+  };
+  auto mma = [&](const f4* fa, const f4* fb) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -655,6 +682,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+  {
+    f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    int pc = pbeg + 16 * wave;
+    if (pc < pend) load(pc, fa0, fb0);
+    for (; pc < pend; pc += 128) {
+      load(pc + 64, fa1, fb1);
+      mma(fa0, fb0);
+      load(pc + 128, fa0, fb0);
+      mma(fa1, fb1);
+    }
   }
 
   // cross-wave reduction in a fixed order: waves 1..3 park their tiles in LDS
@@ -950,9 +988,10 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   t.tn = ct <= tn_max ? ct : tn_max;
   t.gx = (int)ceil_div(ncol4, 16 * t.tn);
   int64_t tiles = (int64_t)t.gx * t.gy;
-  // ~1024 workgroups (4 waves each), at least 1024 pixels (16 chunks per wave) each
+  // ~1024 workgroups (4 waves each), at least 256 pixels (4 chunks per wave) each: small
+  // layers get enough workgroups in flight to hide the load latency
   int64_t want = ceil_div(1024, tiles);
-  int64_t maxs = ceil_div(P, 1024);
+  int64_t maxs = ceil_div(P, 256);
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;
   t.px_split = (int)(ceil_div(ceil_div(P, s), 64) * 64);
@@ -1270,41 +1309,54 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
   if (dconv_use(dyd, dxd, k, stride, pad, dy))
     return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
                         nullptr, dx, dxd, beta, nullptr, true, as_stream(stream), fn);
-  // One launch per (ph, pw) stride-parity class of the input pixels: input row
-  // ih = stride*i + ph receives from output row oh = (ih + pad - kh)/stride for every
-  // kh with (ph + pad - kh) % stride == 0.
+  // Stride-parity classes (ph, pw) of the input pixels: input row ih = stride*i + ph
+  // receives from output row oh = (ih + pad - kh)/stride for every kh with
+  // (ph + pad - kh) % stride == 0.  All classes run in one launch (class = blockIdx.z);
+  // each has only its valid taps.
+  IGemm p{};
+  p.a = dy; p.a_ps = (int)dyd->ps; p.a_c = (int)dyd->c; p.a_c4 = round_up((int)dyd->c, 4);
+  p.a_h = (int)dyd->h; p.a_w = (int)dyd->w;
+  p.g_n = (int)dxd->n;
+  p.a_step = 1;
+  p.dhs = -1; p.dws = -1;
+  p.khs = stride; p.kws = stride; p.ksz = k;
+  p.w = wp; p.n = (int)dxd->c;
+  p.a_bytes = act_bytes(dyd);
+  p.w_bytes = (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4);
+  p.bias = nullptr;
+  p.y = dx; p.y_ps = (int)dxd->ps; p.y_h = (int)dxd->h; p.y_w = (int)dxd->w;
+  p.y_step = stride;
+  p.beta = beta;
+  p.stats = nullptr;
+  int ncls = 0;
   for (int ph = 0; ph < stride; ++ph) {
     for (int pw = 0; pw < stride; ++pw) {
       int gh = (int)((dxd->h - ph + stride - 1) / stride);
       int gw = (int)((dxd->w - pw + stride - 1) / stride);
       if (gh <= 0 || gw <= 0) continue;
+      VAE2_REQUIRE(ncls < 4, fn, "stride > 2 is not supported");
       int kh0 = ((ph + pad) % stride + stride) % stride;
       int kw0 = ((pw + pad) % stride + stride) % stride;
       int nth = kh0 < k ? (k - 1 - kh0) / stride + 1 : 0;
       int ntw = kw0 < k ? (k - 1 - kw0) / stride + 1 : 0;
-      IGemm p{};
-      p.a = dy; p.a_ps = (int)dyd->ps; p.a_c = (int)dyd->c; p.a_c4 = round_up((int)dyd->c, 4);
-      p.a_h = (int)dyd->h; p.a_w = (int)dyd->w;
-      p.g_n = (int)dxd->n; p.g_h = gh; p.g_w = gw;
-      p.a_step = 1;
-      p.nth = nth; p.ntw = ntw;
-      p.dh0 = (ph + pad - kh0) / stride; p.dhs = -1;
-      p.dw0 = (pw + pad - kw0) / stride; p.dws = -1;
-      p.kh0 = kh0; p.khs = stride; p.kw0 = kw0; p.kws = stride; p.ksz = k;
-      p.w = wp; p.n = (int)dxd->c;
-      p.a_bytes = act_bytes(dyd);
-      p.w_bytes = (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4);
-      p.bias = nullptr;
-      p.y = dx; p.y_ps = (int)dxd->ps; p.y_h = (int)dxd->h; p.y_w = (int)dxd->w;
-      p.y_step = stride; p.y_offh = ph; p.y_offw = pw;
-      p.beta = beta;
-      p.stats = nullptr;
-      if (nth == 0 || ntw == 0) { p.nth = 0; p.ntw = 1; }
-      int rc = launch_igemm(p, 1, as_stream(stream), fn);
-      if (rc) return rc;
+      IGemm::Cls& c = p.cls[ncls++];
+      c.g_h = gh; c.g_w = gw;
+      c.nth = nth; c.ntw = ntw;
+      c.dh0 = (ph + pad - kh0) / stride;
+      c.dw0 = (pw + pad - kw0) / stride;
+      c.kh0 = kh0; c.kw0 = kw0;
+      c.y_offh = ph; c.y_offw = pw;
+      if (nth == 0 || ntw == 0) { c.nth = 0; c.ntw = 1; }
     }
   }
-  return 0;
+  if (ncls == 0) return 0;
+  {
+    const IGemm::Cls& c = p.cls[0];  // the single-class launch reads the plain fields
+    p.g_h = c.g_h; p.g_w = c.g_w; p.nth = c.nth; p.ntw = c.ntw;
+    p.dh0 = c.dh0; p.dw0 = c.dw0; p.kh0 = c.kh0; p.kw0 = c.kw0;
+    p.y_offh = c.y_offh; p.y_offw = c.y_offw;
+  }
+  return launch_igemm(p, 1, as_stream(stream), fn, ncls);
 }
 
 int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, int k) {

@@ -31,6 +31,22 @@ SHAPES = [  # H, W, Cin, Cout, k, stride, count per step (App. B, fwd)
     (128, 256, 18, 36, 3, 2, 24),
 ]
 
+# Every ELBO conv shape except the per-branch heads: input H, W.
+ALL_SHAPES = [
+    (128, 256, 18, 64, 3, 1, 1), (128, 256, 64, 64, 3, 1, 12), (128, 256, 64, 64, 1, 1, 4),
+    (128, 256, 64, 256, 1, 1, 12), (128, 256, 256, 64, 1, 1, 4), (128, 256, 256, 18, 3, 1, 4),
+    (128, 256, 256, 36, 3, 2, 4), (128, 256, 18, 18, 3, 1, 96), (128, 256, 18, 36, 3, 2, 24),
+    (128, 256, 18, 18, 3, 2, 28), (128, 256, 9, 64, 3, 1, 3), (128, 256, 38, 18, 3, 1, 1),
+    (128, 256, 28, 18, 3, 1, 2), (64, 128, 36, 36, 3, 1, 96), (64, 128, 36, 18, 1, 1, 24),
+    (64, 128, 36, 72, 3, 2, 24), (64, 128, 18, 72, 3, 2, 20), (64, 128, 18, 18, 3, 2, 8),
+    (64, 128, 36, 36, 3, 2, 8), (64, 128, 56, 36, 3, 1, 1), (64, 128, 46, 36, 3, 1, 2),
+    (32, 64, 72, 72, 3, 1, 80), (32, 64, 72, 18, 1, 1, 20), (32, 64, 72, 36, 1, 1, 20),
+    (32, 64, 72, 144, 3, 2, 12), (32, 64, 18, 144, 3, 2, 8), (32, 64, 36, 144, 3, 2, 8),
+    (32, 64, 92, 72, 3, 1, 1), (32, 64, 82, 72, 3, 1, 2), (16, 32, 144, 144, 3, 1, 32),
+    (16, 32, 144, 18, 1, 1, 8), (16, 32, 144, 36, 1, 1, 8), (16, 32, 144, 72, 1, 1, 8),
+    (16, 32, 164, 144, 3, 1, 1), (16, 32, 154, 144, 3, 1, 2),
+]
+
 
 def timeit(fn, iters):
     s = torch.cuda.Event(enable_timing=True)
@@ -52,7 +68,10 @@ def main():
     ap.add_argument("--only", type=int, nargs="*", help="indices into SHAPES")
     ap.add_argument("--algo", type=int, nargs="*", default=[0],
                     help="vae2_conv2d_set_algo values to compare (0 auto, 1 gather, 2 direct)")
+    ap.add_argument("--all", action="store_true", help="every ELBO conv shape (ALL_SHAPES)")
     a = ap.parse_args()
+    if a.all:
+        SHAPES[:] = ALL_SHAPES
     lib = _lib.load()
     warm = torch.randn(4096, 4096, device="cuda")
     for _ in range(200):  # bring the clocks up before the first timed shape
@@ -67,6 +86,7 @@ def main():
 def run(a, lib):
     dev = "cuda"
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    rows = []
     print(f"{'shape':34s} {'fwd us':>8s} {'TF/s':>6s} {'dgrad us':>9s} {'TF/s':>6s} "
           f"{'wgrad us':>9s} {'TF/s':>6s}")
     for idx, (H, W, ci, co, k, st, cnt) in enumerate(SHAPES):
@@ -113,6 +133,10 @@ def run(a, lib):
         name = f"{H}x{W} {ci}->{co} k{k}s{st} x{cnt}"
         print(f"{name:34s} {tf:8.1f} {flops / tf / 1e6:6.1f} {td:9.1f} {flops / td / 1e6:6.1f} "
               f"{tw:9.1f} {flops / tw / 1e6:6.1f}", flush=True)
+        rows.append((cnt * (tf + td + tw) / 1e3, cnt * tf / 1e3, cnt * td / 1e3, cnt * tw / 1e3, name))
+    print("per-step ms by shape (total, fwd, dgrad, wgrad):")
+    for r in sorted(rows, reverse=True):
+        print(f"  {r[4]:34s} {r[0]:7.2f} {r[1]:7.2f} {r[2]:7.2f} {r[3]:7.2f}")
     print("weighted per-step ms (listed shapes only):",
           {k_: round(v / 1e3, 2) for k_, v in tot.items()})
 
