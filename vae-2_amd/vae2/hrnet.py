@@ -57,8 +57,13 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def run(self, x):
-        out = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
-        sc = x if self.downsample is None else _run_convbn_seq(self.downsample, x)
+        # x feeds conv1 and the shortcut: its two gradient contributions are summed in
+        # the producing kernels (ops.GradLink), not by an autograd add
+        link = ops.GradLink(2)
+        out = ops.conv_bn(x, self.conv1, self.bn1, relu=True, x_link=link)
+        if self.downsample is None:
+            return ops.conv_bn(out, self.conv2, self.bn2, relu=True, residual=x, res_link=link)
+        sc = _run_convbn_seq(self.downsample, x, link)
         return ops.conv_bn(out, self.conv2, self.bn2, relu=True, residual=sc)
 
 
@@ -80,18 +85,21 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def run(self, x):
-        out = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
+        link = ops.GradLink(2)  # x feeds conv1 and the shortcut (see BasicBlock.run)
+        out = ops.conv_bn(x, self.conv1, self.bn1, relu=True, x_link=link)
         out = ops.conv_bn(out, self.conv2, self.bn2, relu=True)
-        sc = x if self.downsample is None else _run_convbn_seq(self.downsample, x)
+        if self.downsample is None:
+            return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=x, res_link=link)
+        sc = _run_convbn_seq(self.downsample, x, link)
         return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=sc)
 
 
 BLOCKS = {"BASIC": BasicBlock, "BOTTLENECK": Bottleneck}
 
 
-def _run_convbn_seq(seq, x):
+def _run_convbn_seq(seq, x, x_link=None):
     """Sequential(Conv2d, BatchNorm2d[, ReLU])."""
-    return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2)
+    return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2, x_link=x_link)
 
 
 def _shortcut(cin, cout, stride):

@@ -106,16 +106,37 @@ def _all_reduce_sums(sums, count, group):
     if group is None:
         return sums, count
     from . import dist as vdist
-    out = sums.clone()
-    vdist.all_reduce_(out, group=group)
-    return out, count * dist.get_world_size(group)
+    vdist.all_reduce_(sums, group=group)  # in place: the callers' sums are fresh buffers
+    return sums, count * dist.get_world_size(group)
+
+
+class GradLink:
+    """In-kernel accumulation of the gradient of a tensor with `n` consumers inside one
+    block (a residual block's input feeds conv1 and the shortcut).  Each consumer's
+    backward writes its contribution into one shared buffer (the first overwrites, the
+    others accumulate with beta = 1 in the producing kernel's epilogue) and only the
+    last one hands the buffer to autograd (the others return None), so autograd never
+    launches an add kernel for it.  Order-agnostic: whichever consumer runs last returns."""
+
+    __slots__ = ("n", "buf", "done")
+
+    def __init__(self, n=2):
+        self.n, self.buf, self.done = n, None, 0
+
+    def finish(self):
+        self.done += 1
+        if self.done < self.n:
+            return None
+        buf, self.buf = self.buf, None
+        return buf
 
 
 # --------------------------------------------------------------- conv + BN ----
 class ConvSpec:
     """Static description of a conv(+BN) call: geometry and module handles."""
 
-    __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training")
+    __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training", "x_link",
+                 "res_link")
 
     def __init__(self, conv, bn=None, relu=False):
         kh, kw = conv.kernel_size
@@ -126,6 +147,7 @@ class ConvSpec:
         self.k, self.stride, self.pad = kh, conv.stride[0], conv.padding[0]
         self.relu = relu
         self.bn = bn
+        self.x_link = self.res_link = None
         if bn is not None:
             if bn.momentum is None:
                 raise ValueError("cumulative-average BatchNorm (momentum=None) is not supported")
@@ -284,11 +306,20 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx):
              ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
     dx = None
     if need_dx:
-        dx = new_act(tuple(x.shape), x)
+        link = spec.x_link
+        beta = 0.0
+        if link is not None and link.buf is not None:
+            dx, beta = link.buf, 1.0  # accumulate onto the other consumer's contribution
+        else:
+            dx = new_act(tuple(x.shape), x)
+            if link is not None:
+                link.buf = dx
         dxp, dxa = act_of(dx)
         wp = packed_weight(weight, 1)
         call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp, ctypes.byref(dxa),
-             spec.k, spec.stride, spec.pad, 0.0, s)
+             spec.k, spec.stride, spec.pad, beta, s)
+        if link is not None:
+            dx = link.finish()
     return dx, wret, bret
 
 
@@ -381,6 +412,7 @@ class _ConvBN(torch.autograd.Function):
         dr = new_act(tuple(r.shape), r)
         drp, dra = act_of(dr)
         dres = None
+        link = spec.res_link
         if ctx.has_res and ctx.needs_input_grad[5]:
             dres = new_act(tuple(r.shape), r)
             dresp, dresa = act_of(dres)
@@ -389,13 +421,21 @@ class _ConvBN(torch.autograd.Function):
         call("vae2_bn_relu_bwd_apply", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
              ctypes.byref(ra), ptr(save), ptr(gamma), ptr(gsums), ctx.count, int(spec.relu), drp,
              ctypes.byref(dra), dresp, ctypes.byref(dresa), s)
+        if dres is not None and link is not None:
+            if link.buf is None:
+                link.buf = dres
+            else:  # (not reached by the blocks: conv1's backward runs after this one)
+                link.buf.add_(dres)
+            dres = link.finish()
         dx, wret, bret_conv = _conv_bwd(x, weight, bias, dr, spec, ctx.needs_input_grad[0])
         return dx, wret, bret_conv, gret, bret, dres, None
 
 
-def conv_bn(x, conv, bn, relu, residual=None):
-    """relu?(bn(conv(x)) + residual) with training-mode (or eval-mode) BatchNorm."""
+def conv_bn(x, conv, bn, relu, residual=None, x_link=None, res_link=None):
+    """relu?(bn(conv(x)) + residual) with training-mode (or eval-mode) BatchNorm.
+    x_link / res_link: GradLink shared with the other consumer(s) of x / residual."""
     spec = ConvSpec(conv, bn, relu)
+    spec.x_link, spec.res_link = x_link, res_link
     return _ConvBN.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec)
 
 
