@@ -239,14 +239,15 @@ def test_up_cat(shapes):
         assert rel(nchw(a.grad), b.grad) < 1e-5
 
 
-def test_fuse_sum_relu():
+@pytest.mark.parametrize("c,sizes", [(8, [(16, 12), (16, 12), (8, 6), (2, 2)]),
+                                     (18, [(16, 32), (8, 16), (2, 4), (1, 1)])])
+def test_fuse_sum_relu(c, sizes):
+    """Includes 18 channels (a padded channel quad in the vectorised adjoint), x8
+    upsampling and a 1x1 source (a window wider than the adjoint's unrolled one)."""
     from vae2 import ops
     torch.manual_seed(4)
-    hw = (16, 12)
-    terms = [torch.randn(2, 8, 16, 12, requires_grad=True),
-             torch.randn(2, 8, 16, 12, requires_grad=True),
-             torch.randn(2, 8, 8, 6, requires_grad=True),
-             torch.randn(2, 8, 2, 2, requires_grad=True)]
+    hw = sizes[0]
+    terms = [torch.randn(2, c, h, w, requires_grad=True) for h, w in sizes]
     y = terms[0]
     for tt in terms[1:]:
         y = y + (tt if tt.shape[-2:] == hw else F.interpolate(tt, size=list(hw), mode="bilinear"))

@@ -116,6 +116,79 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
   }
 }
 
+// The same adjoint, one thread per (input pixel, channel quad): 16-byte loads of dy
+// (pixel strides are multiples of 4 floats) and the column weights of the window
+// computed once per thread instead of once per (row, column).  Same summation order
+// as upsample_bwd_kernel (row sums over ascending columns, then rows).  Windows wider
+// than kUpW columns take the generic loop.
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int kUpW = 24;
+
+__global__ __launch_bounds__(256) void upsample_bwd4_kernel(const float* __restrict__ dy, Act dyd,
+                                                            float* __restrict__ dx, Act dxd,
+                                                            float beta, FastDiv qdiv,
+                                                            FastDiv wdiv, FastDiv hdiv) {
+  const uint32_t C = (uint32_t)dxd.c, Q = (C + 3) / 4;
+  const uint32_t total = (uint32_t)(dxd.n * dxd.h * dxd.w) * Q;
+  const float sh = (float)dxd.h / (float)dyd.h;
+  const float sw = (float)dxd.w / (float)dyd.w;
+  const int OH = (int)dyd.h, OW = (int)dyd.w;
+  const int64_t ps = dyd.ps;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t p = qdiv.div(i);
+    const uint32_t c = 4 * (i - p * Q);
+    const uint32_t row = wdiv.div(p);
+    const int ix = (int)(p - row * (uint32_t)dxd.w);
+    const uint32_t n = hdiv.div(row);
+    const int iy = (int)(row - n * (uint32_t)dxd.h);
+    int ylo = (int)floorf(((float)iy - 0.5f) / sh - 0.5f) - 1;
+    int yhi = (int)ceilf(((float)iy + 1.5f) / sh - 0.5f) + 1;
+    int xlo = (int)floorf(((float)ix - 0.5f) / sw - 0.5f) - 1;
+    int xhi = (int)ceilf(((float)ix + 1.5f) / sw - 0.5f) + 1;
+    if (ylo < 0) ylo = 0;
+    if (xlo < 0) xlo = 0;
+    if (yhi > OH - 1) yhi = OH - 1;
+    if (xhi > OW - 1) xhi = OW - 1;
+    if (iy == (int)dxd.h - 1) yhi = OH - 1;
+    if (ix == (int)dxd.w - 1) xhi = OW - 1;
+    const float* base = dy + (int64_t)n * OH * OW * ps + c;
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    if (xhi - xlo < kUpW) {
+      float wx[kUpW];
+#pragma unroll
+      for (int k = 0; k < kUpW; ++k)
+        wx[k] = (xlo + k <= xhi) ? lerp_weight(xlo + k, (int)dxd.w, sw, ix) : 0.f;
+      for (int oy = ylo; oy <= yhi; ++oy) {
+        const float wy = lerp_weight(oy, (int)dxd.h, sh, iy);
+        if (wy == 0.f) continue;
+        const float* rp = base + ((int64_t)oy * OW + xlo) * ps;
+        f4v ax = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < kUpW; ++k)
+          if (wx[k] != 0.f) ax += wx[k] * *reinterpret_cast<const f4v*>(rp + k * ps);
+        acc += wy * ax;
+      }
+    } else {
+      for (int oy = ylo; oy <= yhi; ++oy) {
+        const float wy = lerp_weight(oy, (int)dxd.h, sh, iy);
+        if (wy == 0.f) continue;
+        f4v ax = {0.f, 0.f, 0.f, 0.f};
+        for (int ox = xlo; ox <= xhi; ++ox) {
+          const float wxv = lerp_weight(ox, (int)dxd.w, sw, ix);
+          if (wxv == 0.f) continue;
+          ax += wxv * *reinterpret_cast<const f4v*>(base + ((int64_t)oy * OW + ox) * ps);
+        }
+        acc += wy * ax;
+      }
+    }
+    float* dst = dx + (int64_t)p * dxd.ps + c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < C) dst[k] = (beta != 0.f) ? acc[k] + beta * dst[k] : acc[k];
+  }
+}
+
 struct FuseTerms {
   const float* x[4];
   Act d[4];
@@ -348,6 +421,14 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
   int64_t total = act_elems(dxd);
   VAE2_REQUIRE(total < (int64_t(1) << 31) && act_elems(dyd) < (int64_t(1) << 31), fn,
                "tensor too large");
+  if (dyd->ps % 4 == 0 && (uintptr_t)dy % 16 == 0) {
+    const int64_t quads = act_elems(dxd) / dxd->c * ((dxd->c + 3) / 4);
+    hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(ew_blocks(quads)), dim3(256), 0,
+                       as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
+                       FastDiv((uint32_t)((dxd->c + 3) / 4)), FastDiv((uint32_t)dxd->w),
+                       FastDiv((uint32_t)dxd->h));
+    return check_launch(fn);
+  }
   hipLaunchKernelGGL(upsample_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
                      FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)dxd->w),
