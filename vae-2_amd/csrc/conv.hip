@@ -941,30 +941,33 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
 }
 
 // dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin4 + ci]
-// Block = 4 waves x 64 slab columns: lane = column (coalesced 256-B rows per split),
-// wave w sums splits w, w+4, ...; the 4 partial sums are combined in LDS in order.
+// Block = 32 slab columns x 8 split groups: thread (g, col) sums splits g, g+8, ...
+// (unrolled: its loads are independent), the 8 group sums are combined in LDS in a fixed
+// order (deterministic).  Small slabs still get ceil(slab/32) blocks and short chains.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                            int splits, int cout, int cin,
                                                            int cin4, int k,
                                                            float* __restrict__ dw, int64_t ld,
                                                            int accumulate) {
-  __shared__ float red[4][64];
+  __shared__ float red[8][32];
   const int kk = k * k;
   const int ncol4 = kk * cin4;
   const int total = cout * ncol4;  // slab elements
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int idx = blockIdx.x * 64 + lane;
+  const int cl = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const int idx = blockIdx.x * 32 + cl;
   float s = 0.f;
   if (idx < total) {
     const float* src = part + idx;
     const int64_t stride = (int64_t)total;
 #pragma unroll 8
-    for (int sp = wave; sp < splits; sp += 4) s += src[sp * stride];
+    for (int sp = sg; sp < splits; sp += 8) s += src[sp * stride];
   }
-  red[wave][lane] = s;
+  red[sg][cl] = s;
   __syncthreads();
-  if (wave != 0 || idx >= total) return;
-  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  if (sg != 0 || idx >= total) return;
+  s = red[0][cl];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) s += red[j][cl];
   const int co = idx / ncol4;
   const int col = idx - co * ncol4;
   const int t = col / cin4;
@@ -1437,7 +1440,7 @@ int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* d
   }
 reduce:
   int64_t slab = dyd->c * (int64_t)ncol4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 64)), dim3(256), 0, s,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,
                      (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw, dw_ld,
                      accumulate);
   int rc = check_launch(fn);
