@@ -49,7 +49,8 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
 /* Conv algorithm selection (tuning / A-B measurement): 0 = auto, 1 = the gather
  * implicit-GEMM kernel only, 2 = the LDS-tiled direct 3x3 kernel wherever legal
  * (k = 3, stride 1, pad 1, 16-byte aligned input with ps % 4 == 0); + 4 also
- * disables the wide-N tiles of 1x1 convs.  Returns the previous setting.
+ * disables the wide-N tiles of 1x1 convs, + 8 the in-workgroup K split of the
+ * implicit-GEMM kernel for layers with few row tiles.  Returns the previous setting.
  * Process-wide; set it before building stats buffers.                           */
 int vae2_conv2d_set_algo(int algo);
 

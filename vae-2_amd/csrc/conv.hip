@@ -134,7 +134,10 @@ struct IGemm {
   } cls[4];
 };
 
-template <int TM, int TN, bool VEC, int ROLE>
+// KS = 4: in-workgroup K split for layers with too few row tiles to fill the chip: the 4
+// waves share one (16*TM)-row tile, wave w takes K chunks w, w+4, ..., and the partial
+// tiles are summed in LDS in a fixed order (deterministic) before wave 0's epilogue.
+template <int TM, int TN, bool VEC, int ROLE, int KS = 1>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   IGemm p = pin;
   if (gridDim.z > 1) {
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   const int g = lane >> 4, r = lane & 15;
   const int M = p.g_n * p.g_h * p.g_w;
   const int bm = xcd_remap(blockIdx.x, gridDim.x);
-  const int mw = (bm * 4 + wave) * (16 * TM);
+  const int mw = (KS == 1 ? bm * 4 + wave : bm) * (16 * TM);
   const int n0 = blockIdx.y * BN;
   const int kk4 = p.ksz * p.ksz * p.a_c4;
 
@@ -179,8 +182,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
 
   const int ntaps = p.nth * p.ntw;
   const int K = ntaps * p.a_c4;
-  const int nchunks = (K + 15) >> 4;
-  int tt = 0, c0 = 4 * g;
+  const int nchunks = KS == 1 ? (K + 15) >> 4 : (((K + 15) >> 4) + KS - 1 - wave) / KS;
+  int tt = 0, c0 = 4 * g + (KS == 1 ? 0 : 16 * wave);
   while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
   const bool cpad = (p.a_c & 3) != 0;
 
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       fa[i] = v;
     }
     mk = (m1 ? 2 : 0) | (m2 ? 4 : 0) | (m3 ? 8 : 0);
-    c0 += 16;
+    c0 += 16 * KS;
     while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
   };
   // Masking the pad lanes here (not right after the loads) keeps the next chunk's
@@ -254,6 +257,28 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       load(fa0, fb0, mk0);
       mma(fa1, fb1, mk1);
     }
+  }
+
+  if constexpr (KS > 1) {
+    __shared__ float kred[KS - 1][TM * TN * 4][64];
+    if (wave > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) kred[wave - 1][(i * TN + j) * 4 + e][lane] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (wave > 0) return;  // no barrier below on this path
+#pragma unroll
+    for (int w = 0; w < KS - 1; ++w)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] += kred[w][(i * TN + j) * 4 + e][lane];
   }
 
   // ---- epilogue ----
@@ -293,6 +318,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       csum[j] += __shfl_xor(csum[j], 32, 64);
       csq[j] += __shfl_xor(csq[j], 16, 64);
       csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if (KS > 1) {  // wave 0 holds the whole row tile
+      if (g == 0) {
+        const int rows = gridDim.x;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + j * 16 + r;
+          if (n >= p.n) continue;
+          p.stats[bm * p.n + n] = csum[j];
+          p.stats[(rows + bm) * p.n + n] = csq[j];
+        }
+      }
+      return;
     }
     if (g == 0) {
 #pragma unroll
@@ -494,7 +532,13 @@ __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
 // ------------------------------------------------------------ tiling ----
 struct Tile {
   int tm, tn, nblk;
+  int ks = 1;  // in-workgroup K split (igemm_kernel KS)
 };
+
+// Rows per workgroup and the K split: layers whose row tiles would leave the chip with
+// fewer than ~2 waves per SIMD split K over the workgroup's 4 waves instead (when K has
+// at least 16 chunks of 16), giving 4x the workgroups.
+static int64_t igemm_rows_per_block(const Tile& t) { return (t.ks > 1 ? 16 : 64) * t.tm; }
 
 static int g_wide_tiles = 1;
 
@@ -525,11 +569,22 @@ static Tile pick_tile(int64_t M, int N, bool wide = false) {
   return t;
 }
 
-template <int TM, bool VEC, int ROLE>
+static int g_ksplit = 1;  // vae2_conv2d_set_algo bit 8 disables the K split (A/B tests)
+
+static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
+  const bool wide = wide_ok(M, N, taps);
+  Tile t = pick_tile(M, N, wide);
+  const int64_t blocks = ceil_div(M, 64 * t.tm) * t.nblk * ncls;
+  const int chunks = (taps * k4 + 15) / 16;
+  if (g_ksplit && !wide && blocks < 512 && chunks >= 16) t.ks = 4;
+  return t;
+}
+
+template <int TM, bool VEC, int ROLE, int KS = 1>
 static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((igemm_kernel<TM, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
+  case T: hipLaunchKernelGGL((igemm_kernel<TM, T, VEC, ROLE, KS>), grid, dim3(256), 0, s, p); break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
@@ -547,6 +602,12 @@ static void launch_wide(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
 
 template <bool VEC, int ROLE>
 static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
+  if (t.ks > 1) {  // (never with wide tiles: those need >= 65536 rows)
+    if (t.tm == 4) launch_tn<4, VEC, ROLE, 4>(p, t.tn, grid, s);
+    else if (t.tm == 2) launch_tn<2, VEC, ROLE, 4>(p, t.tn, grid, s);
+    else launch_tn<1, VEC, ROLE, 4>(p, t.tn, grid, s);
+    return;
+  }
   if (t.tm == 2 && t.tn > 4) launch_wide<VEC, ROLE>(p, t.tn, grid, s);
   else if (t.tm == 4) launch_tn<4, VEC, ROLE>(p, t.tn, grid, s);
   else if (t.tm == 2) launch_tn<2, VEC, ROLE>(p, t.tn, grid, s);
@@ -571,10 +632,13 @@ static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int n
     }
   }
   if (M == 0) return 0;
-  Tile t = pick_tile(M, p.n, wide_ok(M, p.n, p.nth * p.ntw));
+  int max_taps = p.nth * p.ntw;
+  for (int c = 0; c < ncls && ncls > 1; ++c)
+    if (p.cls[c].nth * p.cls[c].ntw > max_taps) max_taps = p.cls[c].nth * p.cls[c].ntw;
+  Tile t = pick_igemm_tile(M, p.n, max_taps, p.a_c4, ncls);
   p.hw_div = FastDiv((uint32_t)(p.g_h * p.g_w));
   p.w_div = FastDiv((uint32_t)p.g_w);
-  dim3 grid((unsigned)ceil_div(M, 64 * t.tm), (unsigned)t.nblk, (unsigned)ncls);
+  dim3 grid((unsigned)ceil_div(M, igemm_rows_per_block(t)), (unsigned)t.nblk, (unsigned)ncls);
   bool vec = vec_ok(p.a, p.a_ps);
   if (role == 0) {
     if (vec) launch_tm<true, 0>(p, t, grid, s);
@@ -586,9 +650,9 @@ static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int n
   return check_launch(fn);
 }
 
-static int64_t igemm_rows(int64_t M, int N, int taps) {
-  Tile t = pick_tile(M, N, wide_ok(M, N, taps));
-  return ceil_div(M, 64 * t.tm);
+static int64_t igemm_rows(int64_t M, int N, int taps, int k4) {
+  Tile t = pick_igemm_tile(M, N, taps, k4, 1);
+  return ceil_div(M, igemm_rows_per_block(t));
 }
 
 // ------------------------------------------------------------ wgrad ----
@@ -1243,10 +1307,12 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
 }
 
 int vae2_conv2d_set_algo(int algo) {
-  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4);
-  if (algo >= 0 && algo <= 6 && algo != 3) {
-    g_conv_algo = algo & 3;
-    g_wide_tiles = algo < 4;
+  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8);
+  const int a = algo & 7;
+  if (algo >= 0 && algo <= 15 && a <= 6 && a != 3) {
+    g_conv_algo = a & 3;
+    g_wide_tiles = a < 4;
+    g_ksplit = !(algo & 8);
   }
   return prev;
 }
@@ -1255,7 +1321,7 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
                                    int k, int stride, int pad) {
   if (!act_ok(xd) || !act_ok(yd)) return 0;
   if (dconv_use(xd, yd, k, stride, pad, x)) return dconv_rows(xd, yd);
-  return igemm_rows(act_pixels(yd), (int)yd->c, k * k);
+  return igemm_rows(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4));
 }
 
 int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, int stride,
@@ -1266,8 +1332,11 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
     snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
     return 0;
   }
-  Tile t = pick_tile(act_pixels(yd), (int)yd->c, wide_ok(act_pixels(yd), (int)yd->c, k * k));
-  snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0>", t.tm, t.tn);
+  Tile t = pick_igemm_tile(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4), 1);
+  if (t.ks > 1)
+    snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0, %d>", t.tm, t.tn, t.ks);
+  else
+    snprintf(buf, (size_t)len, "igemm_kernel<%d, %d, true, 0>", t.tm, t.tn);
   return 0;
 }
 
