@@ -312,6 +312,16 @@ int vae2_l1_bwd(const float* p, const vae2_act* pd, const float* t,
                 const vae2_act* td, const float* gout, float scale, float* dp,
                 const vae2_act* dpd, float beta, void* stream);
 
+/* LSGAN term (criterion.py:90-103: MSELoss(reduction='sum') against ones for 'real',
+ * zeros for 'fake', divided by the batch): out[0] = scale * sum (x - target)^2,
+ * target = 1 or 0, scale = 1/B (x 0.5 at the call sites, utils.py:114-119, :256-266).
+ * ws: vae2_reduce_ws_size(elements) floats.                                     */
+int vae2_lsgan_fwd(const float* x, const vae2_act* xd, float target, float scale, float* ws,
+                   float* out, void* stream);
+/* dx (+)= 2 * scale * gout[0] * (x - target)   (beta 0: overwrite, 1: accumulate)  */
+int vae2_lsgan_bwd(const float* x, const vae2_act* xd, float target, const float* gout,
+                   float scale, float* dx, const vae2_act* dxd, float beta, void* stream);
+
 /* Reparameterisation + KL (utils.py:85-101, criterion.py:72-87).
  * muvar: act with 2*zc channels (mu = [0,zc), logvar = [zc,2zc)); eps, z: acts
  * with zc channels.  prior != 0: z = eps (prior_sampling).

@@ -18,6 +18,9 @@ the reference's forward semantics:
   HighResolutionNetEDz.forward           enc_hrnet.py:1070-1122
   FullModel_encdec.forward (reparam,     utils.py:67-155
     L1 / KL, loss assembly)              criterion.py:61-87
+  HighResolutionNetDsc (HighResolution-  enc_hrnet.py:464-510, :1125-1154
+    Net.forward + 1-channel head)
+  LSGAN terms / FullModel_D              criterion.py:90-103, utils.py:114-119, :256-276
   Adam step                              tools/train.py:251-261 (torch.optim.Adam)
 
 Parity is pinned by tests/golden/ fixtures generated from the reference itself
@@ -237,6 +240,42 @@ def run_encz(ez, x):
     return _seq(ez.last_layer, _upcat(ys))
 
 
+def run_dsc(d, x):
+    """Discriminator: trunk + stage 4 + upsample/cat + last_layer -> (N, 1, H, W)."""
+    ys = _stage4(d, "", _trunk(d, "", x))
+    return _seq(d.last_layer, _upcat(ys))
+
+
+def lsgan(sample, real):
+    """MSELoss(sum) against ones (real) / zeros (fake), / batch (criterion.py:90-103)."""
+    target = torch.ones_like(sample) if real else torch.zeros_like(sample)
+    return torch.sum((sample - target) ** 2) / sample.shape[0]
+
+
+def _frames(x, clip_length):
+    """The frame slices the reference feeds D_frame: x.shape[1] // clip_length of
+    them, 3 channels each (utils.py:116-118)."""
+    return [x[:, 3 * f:3 * f + 3] for f in range(x.shape[1] // clip_length)]
+
+
+def gan_terms(ds, df, x2p):
+    """Generator LSGAN terms on x2t_hat (utils.py:114-119)."""
+    seq = 0.5 * lsgan(run_dsc(ds, x2p), True)
+    frame = torch.sum(torch.stack([0.5 * lsgan(run_dsc(df, f), True)
+                                   for f in _frames(x2p, ds.clip_length)]))
+    return seq, frame
+
+
+def d_losses(ds, df, x2t, x2p, gan_lambda=1.0):
+    """FullModel_D.forward (utils.py:256-276): [D_all (1,), D_seq, D_frame]."""
+    x2t, x2p = x2t.detach(), x2p.detach()
+    seq = 0.5 * lsgan(run_dsc(ds, x2t), True) + 0.5 * lsgan(run_dsc(ds, x2p), False)
+    real = [0.5 * lsgan(run_dsc(df, f), True) for f in _frames(x2t, ds.clip_length)]
+    fake = [0.5 * lsgan(run_dsc(df, f), False) for f in _frames(x2p, ds.clip_length)]
+    frame = torch.sum(torch.stack(real)) + torch.sum(torch.stack(fake))
+    return [torch.unsqueeze(gan_lambda * (seq + frame), 0), seq, frame]
+
+
 def l1(p, t):
     return torch.sum(torch.abs(p - t)) / p.shape[0]
 
@@ -251,8 +290,11 @@ def kl(mu, logvar):
 
 
 def elbo(ez, ed, xt, x2t, x3t, eps, code, lambdas=(1.0, 0.1, 1.0), multiplier=1.0,
-         is_baseline=False, baseline_mode="VAE_NATIVE", prior=False):
-    """Reference ELBO step with explicit noise. Returns (terms dict, preds tuple, aux dict)."""
+         is_baseline=False, baseline_mode="VAE_NATIVE", prior=False, ds=None, df=None,
+         gan_lambda=0.0):
+    """Reference ELBO step with explicit noise. Returns (terms dict, preds tuple, aux dict).
+    With discriminators (ds, df) the LSGAN terms are formed as the reference does
+    (always in non-baseline mode, in baseline only for VAE_GAN) and weighted by gan_lambda."""
     l1w, l2w, l3w = lambdas
     kl_w = l3w * multiplier if baseline_mode == "VAE_ANNEAL" else l3w
     aux = {}
@@ -277,11 +319,17 @@ def elbo(ez, ed, xt, x2t, x3t, eps, code, lambdas=(1.0, 0.1, 1.0), multiplier=1.
         t = {"xt_recon": l1(x1p, xt), "x2t_recon": l1(x2p, x2t), "x3t_recon": l1(x3p, x3t),
              "z_KL": kl(mus, logvars)}
         total = l1w * t["xt_recon"] + l2w * t["x2t_recon"] + l3w * t["x3t_recon"] + kl_w * t["z_KL"]
+        if ds is not None:
+            t["gan_seq"], t["gan_frame"] = gan_terms(ds, df, x2p)
+            total = total + gan_lambda * (t["gan_seq"] + t["gan_frame"])
     else:
         t = {"x2t_recon": l1(x2p, x3t)}
         total = l2w * t["x2t_recon"]
         if baseline_mode != "DETERMINISTIC":
             t["z_KL"] = kl(mus, logvars)
             total = total + kl_w * t["z_KL"]
+        if baseline_mode == "VAE_GAN" and ds is not None:
+            t["gan_seq"], t["gan_frame"] = gan_terms(ds, df, x2p)
+            total = total + gan_lambda * (t["gan_seq"] + t["gan_frame"])
     t["loss_all"] = total
     return t, (x1p, x2p, x3p), aux

@@ -17,6 +17,18 @@ Cases
   tiny_base     IS_BASELINE=True, VAE_NATIVE (decoders under no_grad, L1(x2t_hat, x3t))
   w18           HRNet-W18-small-v2, 32x32, B=2, Z=10: outputs, losses, per-parameter
                 gradient norms, init checksums (weights regenerate from the seed)
+  tiny_anneal   VAE_ANNEAL with multiplier 0.37 (KL weight = X3RECON_LAMBDA * multiplier,
+                utils.py:74), full gradients
+  tiny_det      IS_BASELINE + DETERMINISTIC (no posterior net, no code maps, KL = 0;
+                utils.py:76,102-103,128-131; train.py:80 builds no encz), full gradients
+  tiny_prior    sampling_mode='prior_sampling' (z ~ N(0, I) drawn in place of eps,
+                utils.py:88-89,97-98), full gradients
+  tiny_gan      GAN_LAMBDA 1: one full adversarial_train iteration (function.py:491-512):
+                G step with the LSGAN terms through both discriminators (utils.py:114-119),
+                Adam, then the D step (FullModel_D, utils.py:256-276) and its Adam;
+                G and D gradients, D losses, running statistics, parameter sums
+
+    python tests/golden/make_golden.py [case ...]   # default: all cases
 """
 import os
 import sys
@@ -74,24 +86,28 @@ def checksums(sd):
 
 
 def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, W=32,
-             full_grads=False, adam_steps=0, z=None):
+             full_grads=False, adam_steps=0, z=None, multiplier=1.0, sampling="default",
+             gan=0.0):
     import torch
     import models.enc_hrnet as eh
     from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
-    from utils.utils import FullModel_encdec
+    from utils.utils import FullModel_D, FullModel_encdec
 
     cfg = make_cfg(tiny, hd, baseline, mode, z=z)
     L = cfg.TRAIN.CLIP_LENGTH
     zc = cfg.MODEL.EXTRA.Z_DIM
-    torch.manual_seed(0)
+    det = mode == "DETERMINISTIC"
+    torch.manual_seed(0)  # construction order of train.py:79-82
     ed = eh.get_encdec_model(cfg)
-    ez = eh.get_encz_model(cfg)
+    ez = eh.get_encz_model(cfg) if not det else None
     ds = eh.get_D_sequence_model(cfg)
     df = eh.get_D_frame_model(cfg)
     init_ed = {k: v.clone() for k, v in ed.state_dict().items()}
-    init_ez = {k: v.clone() for k, v in ez.state_dict().items()}
+    init_ez = {k: v.clone() for k, v in ez.state_dict().items()} if ez is not None else {}
+    init_ds = {k: v.clone() for k, v in ds.state_dict().items()}
+    init_df = {k: v.clone() for k, v in df.state_dict().items()}
     fm = FullModel_encdec(ez, ed, ds, df, L1Loss(), KLLoss(), lsgan_adversarial_loss(),
-                          1.0, 0.1, 1.0, 0.0)
+                          1.0, 0.1, 1.0, gan)
     fm.train()
     g = torch.Generator().manual_seed(1)
     xt, x2t, x3t = [torch.randn(B, 3 * L, H, W, generator=g) for _ in range(3)]
@@ -108,20 +124,23 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
         r = ed_fwd(x, z=z, is_baseline=is_baseline)
         return r
     ed.forward = ed_hook
-    ez.register_forward_hook(lambda m, i, o: cap.__setitem__(
-        "muvar", [t.detach().clone() for t in o] if isinstance(o, list) else o.detach().clone()))
+    if ez is not None:
+        ez.register_forward_hook(lambda m, i, o: cap.__setitem__(
+            "muvar", [t.detach().clone() for t in o] if isinstance(o, list) else o.detach().clone()))
 
     torch.manual_seed(123)
-    losses, x1p, x2p, x3p = fm(xt, x2t, x3t, 1.0, is_baseline=baseline, baseline_mode=mode)
+    losses, x1p, x2p, x3p = fm(xt, x2t, x3t, multiplier, is_baseline=baseline, baseline_mode=mode,
+                               sampling_mode=sampling)
     # replay the draws (eps then code; SURVEY.md App. C, verified bit-exact)
     torch.manual_seed(123)
-    if mode != "DETERMINISTIC":
+    if not det:
         if hd:
             eps = [torch.randn(B, zc, m.shape[2], m.shape[3]) for m in cap["muvar"]]
         else:
-            eps = torch.randn(B, zc, 1, 1)
-    code = torch.randn(B, zc, 1, 1)
-    if mode != "DETERMINISTIC":
+            eps = torch.randn(B, zc, 1, 1)  # in prior_sampling: z itself
+        code = torch.randn(B, zc, 1, 1)
+        out["code"] = code
+    if not det:
         if hd:
             for i, e in enumerate(eps):
                 out[f"eps{i}"] = e
@@ -131,14 +150,13 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
             out["eps"] = eps
             out["muvar"] = cap["muvar"]
             out["z"] = cap["ed_z"]
-    out["code"] = code
     out["x1p"], out["x2p"], out["x3p"] = x1p.detach(), x2p.detach(), x3p.detach()
-    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
-    for n, v in zip(names, losses[:5]):
+    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL", "gan_seq", "gan_frame"]
+    for n, v in zip(names, losses):
         out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]) if torch.is_tensor(v) else v)
     losses[0].backward()
-    params = [(n, p) for n, p in list(ez.named_parameters(prefix="encz")) +
-              list(ed.named_parameters(prefix="ed"))]
+    params = [(n, p) for n, p in (list(ez.named_parameters(prefix="encz")) if ez is not None
+                                  else []) + list(ed.named_parameters(prefix="ed"))]
     gnames = [n for n, p in params]
     gnorm = np.array([float(p.grad.double().norm()) if p.grad is not None else 0.0
                       for n, p in params])
@@ -148,16 +166,22 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
             if p.grad is not None:
                 out["grad/" + n] = p.grad.detach().clone()
     # running statistics after one step
-    rs = {("encz." + k): v for k, v in ez.state_dict().items() if "running" in k}
+    rs = {("encz." + k): v for k, v in ez.state_dict().items() if "running" in k} if ez else {}
     rs.update({("ed." + k): v for k, v in ed.state_dict().items() if "running" in k})
     rn, rsum, rabs = checksums(rs)
     out["running_sum"] = torch.as_tensor(rsum)
     out["running_abs"] = torch.as_tensor(rabs)
     # init checksums (weights regenerate from torch.manual_seed(0))
     _, s1, a1 = checksums(init_ed)
-    _, s2, a2 = checksums(init_ez)
     out["init_ed_sum"], out["init_ed_abs"] = torch.as_tensor(s1), torch.as_tensor(a1)
-    out["init_ez_sum"], out["init_ez_abs"] = torch.as_tensor(s2), torch.as_tensor(a2)
+    if ez is not None:
+        _, s2, a2 = checksums(init_ez)
+        out["init_ez_sum"], out["init_ez_abs"] = torch.as_tensor(s2), torch.as_tensor(a2)
+    if gan:
+        for key, sd in (("ds", init_ds), ("df", init_df)):
+            _, s3, a3 = checksums(sd)
+            out[f"init_{key}_sum"], out[f"init_{key}_abs"] = torch.as_tensor(s3), torch.as_tensor(a3)
+        run_d_step(out, fm, ds, df, params, xt, x2t, x2p, lsgan_adversarial_loss, FullModel_D)
     if adam_steps:
         ps = [p for n, p in list(ez.named_parameters()) + list(ed.named_parameters())]
         opt = torch.optim.Adam([{"params": ps}], lr=1e-4)
@@ -183,18 +207,60 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
     print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
 
 
+def run_d_step(out, fm, ds, df, gparams, xt, x2t, x2p, lsgan, FullModel_D):
+    """The rest of one adversarial_train iteration (function.py:499-512): Adam on the
+    generator (encz + ED, 'D_model' excluded, train.py:251-256), then the D step."""
+    import torch
+    opt_g = torch.optim.Adam([{"params": [p for _, p in gparams]}], lr=1e-4)
+    opt_g.step()
+    fmd = FullModel_D(ds, df, lsgan())
+    fmd.train()
+    dparams = list(ds.named_parameters(prefix="ds")) + list(df.named_parameters(prefix="df"))
+    opt_d = torch.optim.Adam([{"params": [p for _, p in dparams]}], lr=1e-4)
+    dl = fmd(x2t=x2t, x2t_predict=x2p.detach())
+    for n, v in zip(("D_all", "D_seq", "D_frame"), dl):
+        out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]))
+    opt_d.zero_grad()
+    dl[0].backward()
+    out["dgrad_norms"] = torch.as_tensor(np.array([float(p.grad.double().norm())
+                                                   for _, p in dparams]))
+    for n, p in dparams:
+        out["dgrad/" + n] = p.grad.detach().clone()
+    opt_d.step()
+    rs = {("ds." + k): v for k, v in ds.state_dict().items() if "running" in k}
+    rs.update({("df." + k): v for k, v in df.state_dict().items() if "running" in k})
+    _, rsum, _ = checksums(rs)
+    out["d_running_sum"] = torch.as_tensor(rsum)
+    _, gsum, _ = checksums({n: p.detach() for n, p in gparams})
+    out["g_param_sum"] = torch.as_tensor(gsum)
+    _, dsum, _ = checksums({n: p.detach() for n, p in dparams})
+    out["d_param_sum"] = torch.as_tensor(dsum)
+    out["dgrad_names"] = np.array([n for n, _ in dparams])
+
+
+CASES = {
+    "tiny_native": dict(tiny=True, full_grads=True, adam_steps=3),
+    # Z_DIM 3: with 2*Z_DIM equal to a branch width the reference's HD_Z z-net has a
+    # None projection and fails (enc_hrnet.py:1018-1019, :1106)
+    "tiny_hdz": dict(tiny=True, hd=True, z=3),
+    "tiny_base": dict(tiny=True, baseline=True),
+    "w18": dict(tiny=False),
+    "tiny_anneal": dict(tiny=True, mode="VAE_ANNEAL", multiplier=0.37, full_grads=True),
+    # DETERMINISTIC is only runnable with IS_BASELINE (non-baseline reads mus, utils.py:113)
+    "tiny_det": dict(tiny=True, baseline=True, mode="DETERMINISTIC", full_grads=True),
+    "tiny_prior": dict(tiny=True, sampling="prior_sampling", full_grads=True),
+    "tiny_gan": dict(tiny=True, gan=1.0, full_grads=True),
+}
+
+
 def main():
     sys.dont_write_bytecode = True
     sys.path.insert(0, REF)
     np.int = int  # the reference uses the removed numpy alias (enc_hrnet.py:321,596,700)
     import torch
     torch.set_num_threads(8)
-    run_case("tiny_native", tiny=True, full_grads=True, adam_steps=3)
-    # Z_DIM 3: with 2*Z_DIM equal to a branch width the reference's HD_Z z-net has a
-    # None projection and fails (enc_hrnet.py:1018-1019, :1106)
-    run_case("tiny_hdz", tiny=True, hd=True, z=3)
-    run_case("tiny_base", tiny=True, baseline=True)
-    run_case("w18", tiny=False)
+    for tag in (sys.argv[1:] or list(CASES)):
+        run_case(tag, **CASES[tag])
 
 
 if __name__ == "__main__":

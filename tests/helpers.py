@@ -42,13 +42,16 @@ def make_cfg(arch="tiny", hd=False, baseline=False, mode="VAE_NATIVE", z=None, L
                     "TRAIN": {"CLIP_LENGTH": L, "IMAGE_SIZE": [hw[1], hw[0]]}})
 
 
-def build(cfg, seed=0):
-    """ED + EDz (+ D models, for RNG order) exactly as tools/train.py builds them."""
+def build(cfg, seed=0, with_d=False):
+    """ED + EDz (+ the two discriminators with with_d) in tools/train.py's construction
+    order (train.py:79-82): returns (ed, ez) or (ed, ez, ds, df)."""
     from vae2 import hrnet
     torch.manual_seed(seed)
     ed = hrnet.get_encdec_model(cfg)
     ez = hrnet.get_encz_model(cfg) if cfg.MODEL.EXTRA.BASELINE_MODE != "DETERMINISTIC" else None
-    return ed, ez
+    if not with_d:
+        return ed, ez
+    return ed, ez, hrnet.get_D_sequence_model(cfg), hrnet.get_D_frame_model(cfg)
 
 
 def golden(name):

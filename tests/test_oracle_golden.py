@@ -93,3 +93,101 @@ def test_oracle_grads_and_adam_match_reference():
     np.testing.assert_allclose(traj, g["adam_losses"], rtol=1e-5)
     psum = np.array([float(p.detach().double().sum()) for _, p in sorted(params)])
     np.testing.assert_allclose(psum, g["adam_param_sum"], rtol=1e-4, atol=1e-6)
+
+
+# ---- ELBO modes and the GAN step (fixtures: make_golden.py tiny_anneal / tiny_det /
+# tiny_prior / tiny_gan) ----
+MODES = {
+    "tiny_anneal": dict(kw=dict(arch="tiny", mode="VAE_ANNEAL"), multiplier=0.37),
+    "tiny_det": dict(kw=dict(arch="tiny", baseline=True, mode="DETERMINISTIC")),
+    "tiny_prior": dict(kw=dict(arch="tiny"), prior=True),
+}
+
+
+def _grad_check(params, g, prefix="grad"):
+    ref_norms = g[prefix + "_norms"]
+    big = ref_norms > 1e-6 * ref_norms.max()  # analytically-zero biases before BN excluded
+    norms = np.array([float(p.grad.double().norm()) if p.grad is not None else 0.0
+                      for _, p in params])
+    np.testing.assert_allclose(norms[big], ref_norms[big], rtol=1e-3)
+    for n, p in params:
+        key = f"{prefix}/{n}"
+        if key in g.files and np.abs(g[key]).max() > 1e-6 * ref_norms.max():
+            assert rel(p.grad, t(g[key])) < 1e-3, n
+
+
+@pytest.mark.parametrize("case", list(MODES))
+def test_oracle_modes_match_reference(case):
+    """VAE_ANNEAL (KL x multiplier), DETERMINISTIC (baseline, no posterior net) and
+    prior sampling (z drawn from N(0, I)): loss terms, predictions and gradients."""
+    torch.set_num_threads(8)
+    spec = MODES[case]
+    kw = spec["kw"]
+    g = golden(case)
+    ed, ez = build(make_cfg(**kw))
+    det = kw.get("mode") == "DETERMINISTIC"
+    assert (ez is None) == det
+    s, a = checksums(ed.state_dict())
+    np.testing.assert_array_equal(s, g["init_ed_sum"])
+    eps = None if det else t(g["eps"])
+    code = None if det else t(g["code"])
+    xt, x2t, x3t = t(g["xt"]), t(g["x2t"]), t(g["x3t"])
+    terms, (x1p, x2p, x3p), _ = ref_cpu.elbo(
+        ez, ed, xt, x2t, x3t, eps, code, multiplier=spec.get("multiplier", 1.0),
+        is_baseline=kw.get("baseline", False), baseline_mode=kw.get("mode", "VAE_NATIVE"),
+        prior=spec.get("prior", False))
+    for name, v in terms.items():
+        ref = float(g["loss_" + name])
+        assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-7, (name, float(v), ref)
+    assert max_rel(x2p, t(g["x2p"])) < 1e-4
+    terms["loss_all"].backward()
+    params = (list(ez.named_parameters(prefix="encz")) if ez is not None else []) + \
+        list(ed.named_parameters(prefix="ed"))
+    assert list(g["grad_names"]) == [n for n, _ in params]
+    _grad_check(params, g)
+
+
+def test_oracle_gan_iteration_matches_reference():
+    """One full adversarial_train iteration with GAN_LAMBDA 1 (function.py:491-512):
+    G losses incl. the LSGAN terms, G gradients, Adam, D losses, D gradients, Adam,
+    discriminator running statistics and parameter sums."""
+    torch.set_num_threads(8)
+    g = golden("tiny_gan")
+    ed, ez, ds, df = build(make_cfg("tiny"), with_d=True)
+    for key, m in (("ds", ds), ("df", df)):
+        s, a = checksums(m.state_dict())
+        np.testing.assert_array_equal(s, g[f"init_{key}_sum"])
+        np.testing.assert_array_equal(a, g[f"init_{key}_abs"])
+    for m in (ed, ez, ds, df):
+        m.train()
+    xt, x2t, x3t = t(g["xt"]), t(g["x2t"]), t(g["x3t"])
+    terms, (x1p, x2p, x3p), _ = ref_cpu.elbo(ez, ed, xt, x2t, x3t, t(g["eps"]), t(g["code"]),
+                                             ds=ds, df=df, gan_lambda=1.0)
+    for name, v in terms.items():
+        ref = float(g["loss_" + name])
+        assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-7, (name, float(v), ref)
+    gparams = list(ez.named_parameters(prefix="encz")) + list(ed.named_parameters(prefix="ed"))
+    opt_g = torch.optim.Adam([p for _, p in gparams], lr=1e-4)
+    opt_g.zero_grad()
+    terms["loss_all"].backward()
+    _grad_check(gparams, g)
+    opt_g.step()
+    dparams = list(ds.named_parameters(prefix="ds")) + list(df.named_parameters(prefix="df"))
+    assert list(g["dgrad_names"]) == [n for n, _ in dparams]
+    opt_d = torch.optim.Adam([p for _, p in dparams], lr=1e-4)
+    dl = ref_cpu.d_losses(ds, df, x2t, x2p)
+    for name, v in zip(("D_all", "D_seq", "D_frame"), dl):
+        ref = float(g["loss_" + name])
+        assert abs(float(v.reshape(-1)[0]) - ref) <= 1e-5 * abs(ref), (name, float(v), ref)
+    opt_d.zero_grad()
+    dl[0].backward()
+    _grad_check(dparams, g, "dgrad")
+    opt_d.step()
+    rs = {("ds." + k): v for k, v in ds.state_dict().items() if "running" in k}
+    rs.update({("df." + k): v for k, v in df.state_dict().items() if "running" in k})
+    # running means of the discriminators sum to ~1e-5 (cancellation): absolute floor
+    np.testing.assert_allclose(checksums(rs)[0], g["d_running_sum"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(checksums({n: p.detach() for n, p in gparams})[0],
+                               g["g_param_sum"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(checksums({n: p.detach() for n, p in dparams})[0],
+                               g["d_param_sum"], rtol=1e-4, atol=1e-6)

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void bn_apply_q_kernel(
     for (int k = 0; k < 4; ++k) {
       float t = __builtin_fmaf(v[u][k], sc[k], sh[k]);
       if (res) t += rv[u][k];
-      o[k] = (relu && !(t > 0.f)) ? 0.f : t;
+      o[k] = (relu && t < 0.f) ? 0.f : t;  // NaN propagates (torch.relu)
     }
     st4(y + p * yd.ps + c, o, c, C);
   }
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
     uint32_t c = i - p * C;
     float v = __builtin_fmaf(x[(int64_t)p * xd.ps + c], scale[c], shift[c]);
     if (res) v += res[(int64_t)p * rd.ps + c];
-    if (relu) v = v > 0.f ? v : 0.f;
+    if (relu) v = v < 0.f ? 0.f : v;
     y[(int64_t)p * yd.ps + c] = v;
   }
 }
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel_v4(
     if (res) v += *reinterpret_cast<const f4*>(res + (int64_t)p * rd.ps + c);
     if (relu) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+      for (int k = 0; k < 4; ++k) v[k] = v[k] < 0.f ? 0.f : v[k];
     }
     *reinterpret_cast<f4*>(y + (int64_t)p * yd.ps + c) = v;
   }

@@ -6,6 +6,8 @@
 //   loss assembly (utils.py:150-152)       -> vae2_weighted_sum
 //   _anomoly_detection (utils.py:63-65)    -> vae2_nonfinite_check
 //   torch.optim.Adam (train.py:251-261)    -> vae2_adam_step
+//   lsgan_adversarial_loss (criterion.py:90-103): MSELoss(sum) vs ones / zeros / batch
+//                                          -> vae2_lsgan_fwd / vae2_lsgan_bwd
 #include "common.h"
 
 namespace vae2 {
@@ -77,6 +79,45 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ p
     float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
     float* dst = dp + (int64_t)px * dpd.ps + c;
     float v = sg * g;
+    *dst = (beta != 0.f) ? v + beta * *dst : v;
+  }
+}
+
+// sum (x - target)^2 partials (target a constant: 1 for 'real', 0 for 'fake')
+__global__ __launch_bounds__(256) void sqdiff_partials_kernel(const float* __restrict__ x, Act xd,
+                                                              float target,
+                                                              float* __restrict__ ws,
+                                                              FastDiv cdiv) {
+  __shared__ float red[4];
+  const uint32_t C = (uint32_t)xd.c;
+  const uint32_t total = (uint32_t)(xd.n * xd.h * xd.w) * C;
+  float s = 0.f;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t px = cdiv.div(i);
+    uint32_t c = i - px * C;
+    const float d = x[(int64_t)px * xd.ps + c] - target;
+    s = __builtin_fmaf(d, d, s);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+// dx (+)= 2 * scale * gout * (x - target)
+__global__ __launch_bounds__(256) void sqdiff_bwd_kernel(const float* __restrict__ x, Act xd,
+                                                         float target,
+                                                         const float* __restrict__ gout,
+                                                         float scale, float* __restrict__ dx,
+                                                         Act dxd, float beta, FastDiv cdiv) {
+  const uint32_t C = (uint32_t)xd.c;
+  const uint32_t total = (uint32_t)(xd.n * xd.h * xd.w) * C;
+  const float g = 2.f * gout[0] * scale;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t px = cdiv.div(i);
+    uint32_t c = i - px * C;
+    const float v = g * (x[(int64_t)px * xd.ps + c] - target);
+    float* dst = dx + (int64_t)px * dxd.ps + c;
     *dst = (beta != 0.f) ? v + beta * *dst : v;
   }
 }
@@ -251,6 +292,35 @@ int vae2_l1_bwd(const float* p, const vae2_act* pd, const float* t,
   hipLaunchKernelGGL(l1_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), p,
                      to_act(pd), t, to_act(td), gout, scale, dp, to_act(dpd), beta,
                      FastDiv((uint32_t)pd->c));
+  return check_launch(fn);
+}
+
+int vae2_lsgan_fwd(const float* x, const vae2_act* xd, float target, float scale, float* ws,
+                   float* out, void* stream) {
+  const char* fn = "vae2_lsgan_fwd";
+  VAE2_REQUIRE(x && ws && out && act_ok(xd), fn, "bad arguments");
+  const int64_t total = act_elems(xd);
+  const unsigned nb = reduce_blocks(total);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(sqdiff_partials_kernel, dim3(nb), dim3(256), 0, s, x, to_act(xd), target,
+                     ws, FastDiv((uint32_t)xd->c));
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
+                     scale, out, 0);
+  return check_launch(fn);
+}
+
+int vae2_lsgan_bwd(const float* x, const vae2_act* xd, float target, const float* gout,
+                   float scale, float* dx, const vae2_act* dxd, float beta, void* stream) {
+  const char* fn = "vae2_lsgan_bwd";
+  VAE2_REQUIRE(x && gout && dx && act_ok(xd) && act_ok(dxd), fn, "bad arguments");
+  VAE2_REQUIRE(dxd->n == xd->n && dxd->h == xd->h && dxd->w == xd->w && dxd->c == xd->c, fn,
+               "dx shape mismatch");
+  const int64_t total = act_elems(xd);
+  hipLaunchKernelGGL(sqdiff_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+                     x, to_act(xd), target, gout, scale, dx, to_act(dxd), beta,
+                     FastDiv((uint32_t)xd->c));
   return check_launch(fn);
 }
 

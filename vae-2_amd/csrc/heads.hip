@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void head_out_fwd_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float h = __builtin_fmaf(v[k], a[k], b[k]);
-        h = (4 * q + k < C && h > 0.f) ? h : 0.f;
+        h = (4 * q + k < C && !(h < 0.f)) ? h : 0.f;  // NaN propagates
 #pragma unroll
         for (int o = 0; o < CO; ++o) acc[o] += h * sw[o * c4 + q][k];
       }
@@ -291,7 +291,6 @@ struct UpSum {
   int y_ps, C;
   float* stats;  // [2][rows][C], row = (n*H + oy)*nxb + xb
   int rows, nxb;
-  int dbg;
 };
 
 template <int NUP>
@@ -319,10 +318,10 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
 #pragma unroll
   for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
     const int k = 4 * kb + g;
-    fa[kb] = (!(p.dbg & 1) && kb < kq && pxa < xn && k < p.cin) ? xrow[(int64_t)pxa * p.x_ps + k] : 0.f;
+    fa[kb] = (kb < kq && pxa < xn && k < p.cin) ? xrow[(int64_t)pxa * p.x_ps + k] : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      fb[kb][j] = (!(p.dbg & 1) && kb < kq) ? p.wp[(int64_t)(c0 + 16 * j + r) * p.cin4 + k] : 0.f;
+      fb[kb][j] = (kb < kq) ? p.wp[(int64_t)(c0 + 16 * j + r) * p.cin4 + k] : 0.f;
   }
   // ---- vertical blends of each source over the chunk's source-column window ----
   constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
@@ -343,7 +342,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
 #pragma unroll
     for (int u = 0; u < VU; ++u) {
       const int ix = vlo[s] + wave + 4 * u;
-      const bool ok = !(p.dbg & 2) && cok && ix <= vhi[s];
+      const bool ok = cok && ix <= vhi[s];
       a0[s][u] = ok ? r0[(int64_t)ix * p.zps[s]] : 0.f;
       a1[s][u] = ok ? r1[(int64_t)ix * p.zps[s]] : 0.f;
     }
@@ -399,7 +398,6 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
       float v = acc[j][e];
 #pragma unroll
       for (int s = 0; s < NUP; ++s) {
-        if (p.dbg & 4) break;
         const float* vj = vs + 16 * j + r;
         v += t[s][2] * vj[__float_as_int(t[s][0])] + t[s][3] * vj[__float_as_int(t[s][1])];
       }
@@ -739,10 +737,6 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   p.stats = stats;
   p.nxb = (int)ceil_div(yd->w, kUsXB);
   p.rows = (int)vae2_conv1x1_upsum_stats_rows(yd);
-  {
-    const char* e = getenv("VAE2_UPSUM_DEBUG");
-    p.dbg = e ? atoi(e) : 0;
-  }
   const int nu = nup > 0 ? nup : 1;
   const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1) * kUsVS) *
                      sizeof(float);

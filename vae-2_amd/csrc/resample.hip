@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* 
                         (float)d.w / (float)yd.w);
       acc = (k == 0) ? v : acc + v;
     }
-    y[(int64_t)p * yd.ps + c] = acc > 0.f ? acc : 0.f;
+    y[(int64_t)p * yd.ps + c] = acc < 0.f ? 0.f : acc;  // NaN propagates (torch.relu)
   }
 }
 

@@ -45,6 +45,7 @@ _SCHEMA = {
         "DEFER_CHECKS": False,    # one NaN/Inf host read per step instead of four
         "SYNTHETIC_DATA": False,  # Cityscapes-shaped Gaussian clips instead of the zip dataset
         "SYNTHETIC_CLIPS": 64,
+        "ELBO_ONLY": False,       # no discriminators / D step (the ELBO step alone)
     },
 }
 

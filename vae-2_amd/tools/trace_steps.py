@@ -1,56 +1,79 @@
 """Per-step kernel-time breakdown from a rocprofv3 kernel trace (CSV).
 
     python vae-2_amd/tools/trace_steps.py gpurun_out/prof/run_kernel_trace.csv [--steps 10]
+        [--instances N] [--json out.json]
 
 Steps are delimited by the Adam launches (the last kernel family of a step).
 Reports, over the last --steps steps: wall span, GPU busy time (union of
-kernel intervals across streams), summed kernel time by family, and the idle gap.
+kernel intervals across streams), summed kernel time per family (conv fwd /
+dgrad, weight-grad, BatchNorm, heads, fuse/resample, ...), per kernel, and the
+top --instances kernel instantiations by time.
 """
 import argparse
 import csv
+import json
 import re
 from collections import defaultdict
 
+FAMILIES = (  # (family, regex on the demangled kernel name), first match wins
+    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false>|igemm_kernel<\d+, \d+, \w+, 0"),
+    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true>|igemm_kernel<\d+, \d+, \w+, [12]"),
+    ("conv_wgrad", r"wgrad"),
+    ("batchnorm", r"bn_|reduce_then|chan_partials|bn_stats|bnfin"),
+    ("heads", r"upsum|head_|up_adj"),
+    ("fuse_resample", r"upsample|fuse_sum|relu_bwd|copy_act|tile_kernel|spatial_|codemap"),
+    ("optimizer", r"adam|pack_weight"),
+    ("loss_elbo", r"l1_|reparam|weighted_sum|finish_sum|scale_kernel|nonfinite|nchw|nhwc"),
+    ("torch_aten", r"at::native|^at::"),
+    ("copies", r"rocclr_copy|rocclr_fill"),
+)
 
-def family(name):
+
+def kernel_name(name):
     n = re.sub(r"^void ", "", name)
     n = re.sub(r"\(.*$", "", n)
-    if n.startswith("vae2::"):
-        n = n[6:]
-    if "igemm_kernel" in n:
-        m = re.search(r"<(\d+), (\d+), (\w+), (\d+)>", n)
-        role = {"0": "conv_fwd", "1": "conv_dgrad", "2": "conv_dgrad_s2"}.get(m.group(4), "igemm")
-        return role
-    n = re.sub(r"<.*", "", n)
-    if "elementwise" in n or n.startswith("at::"):
-        return "torch:" + n.split("::")[-1][:40]
-    return n
+    return n[6:] if n.startswith("vae2::") else n
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("csv")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--marker", default="adam")
-    a = ap.parse_args()
+def short(n):
+    """Kernel without template arguments (aten kernels shortened)."""
+    if "at::native" in n:
+        m = re.search(r"CUDAFunctor_(\w+)|(\w+Functor)|(direct_copy)", n)
+        return "torch:" + (next(g for g in m.groups() if g) if m else n[:40])
+    return re.sub(r"<.*", "", n)
+
+
+def family(n):
+    for f, rx in FAMILIES:
+        if re.search(rx, n):
+            return f
+    return "other"
+
+
+def load(path):
     rows = []
-    with open(a.csv) as f:
+    with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         kernel_name(r["Kernel_Name"])))
     rows.sort()
-    marks = [i for i, r in enumerate(rows) if a.marker in r[2]]
-    # group consecutive marker launches of one step (several flats)
-    ends = []
+    return rows
+
+
+def select_steps(rows, steps, marker="adam"):
+    marks = [i for i, r in enumerate(rows) if marker in r[2]]
+    ends = []  # group consecutive marker launches of one step (several flats)
     for i in marks:
         if ends and i - ends[-1] <= 4:
             ends[-1] = i
         else:
             ends.append(i)
-    if len(ends) < a.steps + 1:
+    if len(ends) < steps + 1:
         raise SystemExit(f"only {len(ends)} steps found")
-    lo, hi = ends[-a.steps - 1] + 1, ends[-1] + 1
-    sel = rows[lo:hi]
-    t0, t1 = sel[0][0], max(r[1] for r in sel)
+    return rows[ends[-steps - 1] + 1:ends[-1] + 1]
+
+
+def busy_ns(sel):
     busy, cur_s, cur_e = 0, None, None
     for s, e, _ in sel:
         if cur_e is None or s > cur_e:
@@ -59,18 +82,49 @@ def main():
             cur_s, cur_e = s, e
         else:
             cur_e = max(cur_e, e)
-    busy += cur_e - cur_s
-    fam = defaultdict(lambda: [0, 0])
+    return busy + (cur_e - cur_s)
+
+
+def breakdown(sel, k):
+    fam, ker, inst = (defaultdict(lambda: [0, 0]) for _ in range(3))
     for s, e, n in sel:
-        f = family(n)
-        fam[f][0] += e - s
-        fam[f][1] += 1
-    k = a.steps
+        for d, key in ((fam, family(n)), (ker, short(n)), (inst, n)):
+            d[key][0] += e - s
+            d[key][1] += 1
+    t0, t1 = sel[0][0], max(r[1] for r in sel)
     total = sum(v[0] for v in fam.values())
-    print(f"steps {k}: wall/step {(t1 - t0) / k / 1e6:.2f} ms, busy/step {busy / k / 1e6:.2f} ms, "
-          f"summed kernel/step {total / k / 1e6:.2f} ms, launches/step {len(sel) / k:.0f}")
-    for f, (t, c) in sorted(fam.items(), key=lambda x: -x[1][0]):
-        print(f"  {f:40s} {t / k / 1e6:8.2f} ms  {c / k:7.0f} launches  {t / c / 1e3:8.1f} us avg")
+
+    def table(d):
+        return [{"name": n, "ms_per_step": t / k / 1e6, "launches_per_step": c / k,
+                 "avg_us": t / c / 1e3} for n, (t, c) in sorted(d.items(), key=lambda x: -x[1][0])]
+
+    return {"steps": k, "wall_ms_per_step": (t1 - t0) / k / 1e6,
+            "busy_ms_per_step": busy_ns(sel) / k / 1e6, "kernel_ms_per_step": total / k / 1e6,
+            "launches_per_step": len(sel) / k, "families": table(fam), "kernels": table(ker),
+            "instances": table(inst)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--marker", default="adam")
+    ap.add_argument("--instances", type=int, default=25)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    b = breakdown(select_steps(load(a.csv), a.steps, a.marker), a.steps)
+    print(f"steps {b['steps']}: wall/step {b['wall_ms_per_step']:.2f} ms, busy/step "
+          f"{b['busy_ms_per_step']:.2f} ms, summed kernel/step {b['kernel_ms_per_step']:.2f} ms, "
+          f"launches/step {b['launches_per_step']:.0f}")
+    for title, key, lim in (("families", "families", None), ("kernels", "kernels", None),
+                            ("top instances", "instances", a.instances)):
+        print(f"-- {title}")
+        for r in b[key][:lim]:
+            print(f"  {r['name'][:60]:60s} {r['ms_per_step']:8.2f} ms  "
+                  f"{r['launches_per_step']:7.1f} launches  {r['avg_us']:8.1f} us avg")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(b, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -12,8 +12,11 @@ file and key names.
 Deliberate differences: `TRAIN.OPTIMIZER: sgd` raises a clear ValueError (the
 reference crashes with a TypeError on `p.name`, train.py:234); single-GPU
 checkpoints are written (the reference calls `.module` on a non-DDP model,
-train.py:322); the GAN / discriminator path (GAN_LAMBDA != 0) is not implemented
-yet; the Cityscapes zip dataset is replaced by MI355X.SYNTHETIC_DATA clips.
+train.py:322); epochs past END_EPOCH use the main loader when no
+DATASET.EXTRA_TRAIN_SET is given (the reference raises a NameError there);
+`MI355X.ELBO_ONLY True` drops the two discriminators (the ELBO step alone; the
+reference always builds them and runs the D step); the Cityscapes zip dataset is
+replaced by MI355X.SYNTHETIC_DATA clips when that switch is set.
 """
 import argparse
 import os
@@ -29,7 +32,7 @@ import models  # noqa: F401
 from config import config, update_config
 from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
 from core.function import adversarial_train
-from utils.utils import FullModel_encdec, create_logger
+from utils.utils import FullModel_D, FullModel_encdec, create_logger
 
 from vae2 import dist as vdist
 from vae2.optim import FusedAdam
@@ -78,10 +81,9 @@ def main(argv=None):
     encdec_model = models.enc_hrnet.get_encdec_model(config)
     encz_model = (models.enc_hrnet.get_encz_model(config)
                   if extra.BASELINE_MODE != "DETERMINISTIC" else None)
-    use_gan = config.TRAIN.GAN_LAMBDA != 0 and (not extra.IS_BASELINE
-                                                 or extra.BASELINE_MODE == "VAE_GAN")
-    D_model_sequence = models.enc_hrnet.get_D_sequence_model(config) if use_gan else None
-    D_model_frame = models.enc_hrnet.get_D_frame_model(config) if use_gan else None
+    use_d = not config.MI355X.ELBO_ONLY
+    D_model_sequence = models.enc_hrnet.get_D_sequence_model(config) if use_d else None
+    D_model_frame = models.enc_hrnet.get_D_frame_model(config) if use_d else None
 
     if args.local_rank == 0:
         this_dir = os.path.dirname(os.path.abspath(__file__))
@@ -111,40 +113,74 @@ def main(argv=None):
         gan_lambda=config.TRAIN.GAN_LAMBDA)
     model_encdec.defer_checks = config.MI355X.DEFER_CHECKS
     model_encdec = model_encdec.to(device)
+    model_D = None
+    if use_d:
+        model_D = FullModel_D(D_model_sequence=D_model_sequence, D_model_frame=D_model_frame,
+                              criterion_gan=lsgan_adversarial_loss()).to(device)
+        assert model_encdec.D_model_sequence is model_D.D_model_sequence, "Unexpected behavior."
+        assert model_encdec.D_model_frame is model_D.D_model_frame, "Unexpected behavior."
+    # Adam over encz + ED ('D_model' excluded) and over the discriminators (train.py:251-261)
     nets = [m for m in (encz_model, encdec_model) if m is not None]
     optimizer = FusedAdam(nets, lr=config.TRAIN.LR)
+    optimizer_D = FusedAdam([D_model_sequence, D_model_frame], lr=config.TRAIN.LR) if use_d \
+        else None
     if vdist.is_dist():  # replicas start identical (DDP's initial broadcast)
-        for f in optimizer.flats:
-            torch.distributed.broadcast(f.data, src=0)
+        for opt in (optimizer, optimizer_D):
+            for f in (opt.flats if opt is not None else []):
+                torch.distributed.broadcast(f.data, src=0)
 
     epoch_iters = int(len(dataset) / config.TRAIN.BATCH_SIZE_PER_GPU / max(1, len(gpus)))
     last_epoch = 0
     state_file = os.path.join(final_output_dir, "checkpoint_encdec.pth.tar")
-    if config.TRAIN.RESUME and os.path.isfile(state_file):
-        ck = torch.load(state_file, map_location="cpu", weights_only=True)
-        last_epoch = ck["epoch"]
-        model_encdec.load_state_dict(ck["state_dict"], strict=False)
-        optimizer.load_state_dict(ck["optimizer_encdec"])
-        logger.info("=> loaded checkpoint (epoch {})".format(ck["epoch"]))
+    state_file_D = os.path.join(final_output_dir, "checkpoint_D.pth.tar")
+    if config.TRAIN.RESUME:  # train.py:270-290
+        if os.path.isfile(state_file):
+            ck = torch.load(state_file, map_location="cpu", weights_only=True)
+            last_epoch = ck["epoch"]
+            model_encdec.load_state_dict(ck["state_dict"], strict=use_d)
+            optimizer.load_state_dict(ck["optimizer_encdec"])
+            logger.info("=> loaded checkpoint (epoch {})".format(ck["epoch"]))
+        if use_d and os.path.isfile(state_file_D):
+            ck = torch.load(state_file_D, map_location="cpu", weights_only=True)
+            last_epoch = ck["epoch"]
+            model_D.load_state_dict(ck["state_dict"])
+            optimizer_D.load_state_dict(ck["optimizer_D"])
+            logger.info("=> loaded checkpoint (epoch {})".format(ck["epoch"]))
 
     start = timeit.default_timer()
     end_epoch = config.TRAIN.END_EPOCH + config.TRAIN.EXTRA_EPOCH
     num_iters = config.TRAIN.END_EPOCH * epoch_iters
+    extra_iters = config.TRAIN.EXTRA_EPOCH * epoch_iters
     for epoch in range(last_epoch, end_epoch):
         if sampler is not None:
             sampler.set_epoch(epoch)
-        adversarial_train(config, epoch, config.TRAIN.END_EPOCH, epoch_iters, config.TRAIN.LR,
-                          num_iters, loader, optimizer, None, model_encdec, None, writer_dict,
-                          device, final_output_dir,
+        if epoch >= config.TRAIN.END_EPOCH:  # extra epochs restart the schedule (train.py:300-306)
+            ep_args = (epoch - config.TRAIN.END_EPOCH, config.TRAIN.EXTRA_EPOCH, epoch_iters,
+                       config.TRAIN.EXTRA_LR, extra_iters, loader)
+            for opt in (optimizer, optimizer_D):
+                if opt is not None:
+                    opt.set_lr(config.TRAIN.EXTRA_LR)
+        else:
+            ep_args = (epoch, config.TRAIN.END_EPOCH, epoch_iters, config.TRAIN.LR, num_iters,
+                       loader)
+        adversarial_train(config, *ep_args, optimizer, optimizer_D, model_encdec, model_D,
+                          writer_dict, device, final_output_dir,
                           use_multiplier=config.TRAIN.USE_X2RECON_MULTIPLIER,
                           is_baseline=extra.IS_BASELINE, baseline_mode=extra.BASELINE_MODE)
-        if vdist.rank() == 0:
+        if vdist.rank() == 0:  # train.py:317-348
             logger.info("=> saving checkpoint to {}".format(state_file))
             torch.save({"epoch": epoch + 1, "state_dict": model_encdec.state_dict(),
                         "optimizer_encdec": optimizer.state_dict()}, state_file)
+            if use_d:
+                logger.info("=> saving checkpoint to {}".format(state_file_D))
+                torch.save({"epoch": epoch + 1, "state_dict": model_D.state_dict(),
+                            "optimizer_D": optimizer_D.state_dict()}, state_file_D)
             if epoch == end_epoch - 1:
                 torch.save(model_encdec.state_dict(),
                            os.path.join(final_output_dir, "model_encdec_final_state.pth"))
+                if use_d:
+                    torch.save(model_D.state_dict(),
+                               os.path.join(final_output_dir, "model_D_final_state.pth"))
                 writer_dict["writer"].close()
                 logger.info("Hours: %d" % int((timeit.default_timer() - start) / 3600))
                 logger.info("Done")

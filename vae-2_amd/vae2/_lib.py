@@ -90,6 +90,8 @@ _SIGS = {
     "vae2_reduce_ws_size": (c_i64, [c_i64]),
     "vae2_l1_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp, c_vp, c_vp]),
     "vae2_l1_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_f32, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_lsgan_fwd": (c_int, [c_vp, P_ACT, c_f32, c_f32, c_vp, c_vp, c_vp]),
+    "vae2_lsgan_bwd": (c_int, [c_vp, P_ACT, c_f32, c_vp, c_f32, c_vp, P_ACT, c_f32, c_vp]),
     "vae2_reparam_kl_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_int, c_f32, c_vp,
                                     c_int, c_vp, c_vp]),
     "vae2_reparam_kl_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, c_f32, c_vp,

@@ -41,7 +41,9 @@ class KLLoss(nn.Module):
 
 
 class lsgan_adversarial_loss(nn.Module):  # noqa: N801 (reference name)
-    """LSGAN loss (criterion.py:90-103): part of the GAN path, SURVEY.md §8f next-1."""
+    """sum (sample - 1)^2 / batch for 'real', sum sample^2 / batch for 'fake'
+    (MSELoss(reduction='sum') against ones / zeros, criterion.py:90-103)."""
 
     def forward(self, sample, mode):
-        raise NotImplementedError("the GAN path (LSGAN + discriminators) is not implemented yet")
+        assert mode in ["real", "fake"]
+        return ops.lsgan(sample, mode == "real", 1.0 / sample.shape[0], flat=True)

@@ -162,8 +162,10 @@ class _Heads(torch.autograd.Function):
         dout = as_act(dout)
         dxs = [None] * nb
         pgrads = []
+        need = ctx.needs_input_grad[2 + nb:]
         for k in range(nh):
             w, b, gamma, beta, w2, b2 = ctx.params[_PER_HEAD * k:_PER_HEAD * (k + 1)]
+            nw, nbias, ng, nbt, nw2, nb2 = need[_PER_HEAD * k:_PER_HEAD * (k + 1)]
             y, save = yv[k], saves[k]
             yp, ya = ptr(y), Act(*ys[0].shape[:3], C, C)
             dk = dout[..., ncls * k:ncls * (k + 1)]
@@ -171,21 +173,21 @@ class _Heads(torch.autograd.Function):
             wsz = lib.vae2_head_out_bwd_ws_size(ctypes.byref(ya), ncls)
             ws = _empty((wsz,), y)
             lsums = _empty((2 * C,), y, torch.float64)
-            gsink, gret = _grad_sink(gamma)
-            btsink, btret = _grad_sink(beta)
-            w2sink, w2ret = _grad_sink(w2)
-            b2sink, b2ret = _grad_sink(b2)
+            gsink, gret = _grad_sink(gamma, ng)
+            btsink, btret = _grad_sink(beta, nbt)
+            w2sink, w2ret = _grad_sink(w2, nw2)
+            b2sink, b2ret = _grad_sink(b2, nb2)
             call("vae2_head_out_bwd_reduce", yp, ctypes.byref(ya), ptr(save), ptr(w2), ncls, dkp,
                  ctypes.byref(dka), ptr(lsums), ptr(gsink), ptr(btsink), ptr(w2sink),
                  ptr(b2sink), ptr(ws), wsz, s)
             gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
             dy = new_act((*ys[0].shape[:3], C), y)
             dyp, dya = act_of(dy)
-            bsink, bret = _grad_sink(b)
+            bsink, bret = _grad_sink(b, nbias)
             call("vae2_head_out_bwd_apply", yp, ctypes.byref(ya), ptr(save), ptr(gamma), ptr(w2),
                  ncls, dkp, ctypes.byref(dka), ptr(gsums), ctx.count, dyp, ctypes.byref(dya),
                  ptr(bsink), ptr(ws), wsz, s)
-            wsink, wret = _grad_sink(w)
+            wsink, wret = _grad_sink(w, nw)
             # dL/dz_j = up_j^T(dL/dy) for every lower branch, dL/dy read once
             gs = [(dy, dyp, dya)]
             for xj in ys[1:]:

@@ -568,9 +568,10 @@ class HighResolutionNetEDz(HighResolutionNet):
 
 
 class HighResolutionNetDsc(HighResolutionNet):
-    """GAN discriminator parameter tree (enc_hrnet.py:1125-1154). Built so that
-    reference checkpoints load; its execution is the next scope item
-     and is not implemented yet."""
+    """GAN discriminator (enc_hrnet.py:1125-1154): the shared trunk with stride-1 stems
+    and one 1-channel head on the upsampled 270-channel concatenation, i.e.
+    HighResolutionNet.forward (:464-510).  Sequence D sees the 3L-channel x2t clip,
+    frame D one RGB frame; the output is a per-pixel score map (N, H, W, 1)."""
 
     def __init__(self, config, is_sequence, **kwargs):
         extra = config.MODEL.EXTRA
@@ -590,16 +591,24 @@ class HighResolutionNetDsc(HighResolutionNet):
         self.last_layer_1 = None
         self.last_layer_2 = None
         self.last_layer_3 = None
+        vheads.mark_split([self.last_layer], self.last_stage_channels)
 
     def _expand_pretrained(self, upd):
         if self.is_sequence and "conv1.weight" in upd:
             return {"conv1.weight": upd["conv1.weight"].repeat([1, self.clip_length, 1, 1])}
         return {}
 
+    def run(self, x):
+        """x: (N,H,W,3L) or (N,H,W,3) NHWC -> D score map (N,H,W,1)."""
+        xs = self._trunk_to_stage4_inputs("", x)
+        ys = run_stage(self.stage4, xs)
+        if vheads.supported([self.last_layer], [int(y.shape[3]) for y in ys]):
+            return vheads.run([self.last_layer], ys)
+        return run_head(self.last_layer, ops.up_cat(ys))
+
     def forward(self, x, *args, **kwargs):
-        raise NotImplementedError(
-            "GAN discriminator execution is not implemented yet (SURVEY.md §8f next-1); "
-            "train the ELBO step with GAN_LAMBDA 0 or without discriminators")
+        """Reference-compatible call on an NCHW tensor -> (N, 1, H, W)."""
+        return ops.to_nchw(self.run(ops.to_nhwc(x)))
 
 
 def get_encdec_model(cfg, **kwargs):

@@ -17,7 +17,19 @@ and copied to the device, so a seeded run reproduces the reference's CPU draws.
 Anomaly checks (utils.py:63-65) keep the reference's AssertionError semantics;
 they are evaluated on a device flag, and `defer_checks=True` postpones the host
 read to `check_anomalies()` (one sync instead of four per step).
+
+GAN terms (utils.py:114-119): with discriminators attached they are formed as the
+reference does (always in non-baseline mode, for VAE_GAN in baseline mode).  The
+reference backpropagates the generator loss into the discriminators too, and the
+D step then zeroes those gradients (function.py:499-510); here the discriminator
+parameters are frozen during the generator pass so no weight gradient is computed
+for them (same results, less work).  With GAN_LAMBDA 0 the terms are evaluated
+without autograd (their gradient is exactly zero).
+
+FullModel_D (utils.py:244-276): the discriminator loss of the D step.
 """
+import contextlib
+
 import torch
 import torch.nn as nn
 
@@ -80,12 +92,19 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
             self._flag.zero_()
             assert not bad, "step got nan or inf"
 
-    def _gan_terms(self):
-        if self.gan_lambda != 0 and self.D_model_sequence is not None:
-            raise NotImplementedError(
-                "GAN terms need the discriminator path (SURVEY.md §8f next-1), not implemented "
-                "yet: set TRAIN.GAN_LAMBDA 0 (ELBO step) or pass D models as None")
-        return 0.0, 0.0
+    def _gan_terms(self, x2p, nframes):
+        """0.5*LSGAN(D_seq(x2t_hat), real), sum_f 0.5*LSGAN(D_frame(frame f), real)."""
+        ds, df = self.D_model_sequence, self.D_model_frame
+        if ds is None or df is None:
+            return 0.0, 0.0
+        B = x2p.shape[0]
+        grad = self.gan_lambda != 0 and torch.is_grad_enabled()
+        with frozen([ds, df]) if grad else torch.no_grad():
+            seq = ops.lsgan(ds.run(x2p), True, 0.5 / B)
+            fl = [ops.lsgan(df.run(f), True, 0.5 / B)
+                  for f in ops.split_frames(x2p, nframes)]
+            frame = ops.weighted_sum(fl, [1.0] * len(fl))
+        return seq, frame
 
     # ---- forward ---------------------------------------------------------------
     def forward(self, xt, x2t, x3t, multiplier, is_baseline=False, baseline_mode="VAE_NATIVE",
@@ -155,9 +174,12 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
             x2t_recon = ops.l1(x2p, x2t_n, scale)
             x3t_recon = ops.l1(x3p, x3t_n, scale)
             z_kl = kl
-            gan_seq, gan_frame = self._gan_terms()
+            gan_seq, gan_frame = self._gan_terms(x2p, x2t.shape[1] // ed.clip_length)
             terms = [xt_recon, x2t_recon, x3t_recon, z_kl]
             lams = [self.x1recon_lambda, self.x2recon_lambda, self.x3recon_lambda, kl_lambda]
+            if torch.is_tensor(gan_seq) and self.gan_lambda != 0:
+                terms += [gan_seq, gan_frame]
+                lams += [self.gan_lambda, self.gan_lambda]
         else:
             xt_recon = 0.0
             x3t_recon = 0.0
@@ -174,8 +196,57 @@ class FullModel_encdec(nn.Module):  # noqa: N801 (reference name)
                 z_kl = kl
                 terms.append(z_kl)
                 lams.append(kl_lambda)
-                gan_seq, gan_frame = self._gan_terms()
+                gan_seq, gan_frame = self._gan_terms(x2p, x2t.shape[1] // ed.clip_length)
+                if torch.is_tensor(gan_seq) and self.gan_lambda != 0:
+                    terms += [gan_seq, gan_frame]
+                    lams += [self.gan_lambda, self.gan_lambda]
         loss_all = ops.weighted_sum(terms, lams)
         preds = (ops.to_nchw(x1p), ops.to_nchw(x2p), ops.to_nchw(x3p))
         return ([torch.unsqueeze(loss_all, 0), xt_recon, x2t_recon, x3t_recon, z_kl, gan_seq,
                  gan_frame], *preds)
+
+
+@contextlib.contextmanager
+def frozen(modules):
+    """Temporarily stop autograd from asking for these modules' parameter gradients."""
+    params = [p for m in modules for p in m.parameters() if p.requires_grad]
+    for p in params:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in params:
+            p.requires_grad_(True)
+
+
+class FullModel_D(nn.Module):  # noqa: N801 (reference name)
+    """Discriminator loss of the D step (utils.py:244-276):
+        D_seq   = 0.5 LSGAN(D_seq(x2t), real) + 0.5 LSGAN(D_seq(x2t_hat), fake)
+        D_frame = sum_f 0.5 LSGAN(D_frame(x2t_f), real) + 0.5 LSGAN(D_frame(x2t_hat_f), fake)
+        D_all   = gan_lambda (D_seq + D_frame)
+    Calls run in the reference's order (BatchNorm running statistics are updated per
+    call).  Returns [D_all (1,), D_seq, D_frame]."""
+
+    def __init__(self, D_model_sequence, D_model_frame, criterion_gan, gan_lambda=1.0):
+        super().__init__()
+        self.D_model_sequence = D_model_sequence
+        self.D_model_frame = D_model_frame
+        self.criterion_gan = criterion_gan
+        self.gan_lambda = gan_lambda
+
+    def forward(self, x2t, x2t_predict):
+        ds, df = self.D_model_sequence, self.D_model_frame
+        B = x2t.shape[0]
+        nframes = x2t.shape[1] // ds.clip_length
+        real = ops.to_nhwc(x2t.detach())
+        fake = ops.to_nhwc(x2t_predict.detach())
+        seq = ops.weighted_sum([ops.lsgan(ds.run(real), True, 0.5 / B),
+                                ops.lsgan(ds.run(fake), False, 0.5 / B)], [1.0, 1.0])
+        fr, ff = [], []
+        for r, f in zip(ops.split_frames(real, nframes), ops.split_frames(fake, nframes)):
+            fr.append(ops.lsgan(df.run(r), True, 0.5 / B))
+            ff.append(ops.lsgan(df.run(f), False, 0.5 / B))
+        frame = ops.weighted_sum([ops.weighted_sum(fr, [1.0] * len(fr)),
+                                  ops.weighted_sum(ff, [1.0] * len(ff))], [1.0, 1.0])
+        d_all = ops.weighted_sum([seq, frame], [self.gan_lambda, self.gan_lambda])
+        return [torch.unsqueeze(d_all, 0), seq, frame]

@@ -20,6 +20,8 @@ Reference operators replaced (see include/vae2_hip.h for the kernel entry points
   avgpool     nn.AdaptiveAvgPool2d((1, 1)) :1025
   l1          L1Loss criterion.py:61-69
   reparam_kl  z = mu + exp(0.5 logvar) eps (utils.py:85-101) + KLLoss criterion.py:72-87
+  lsgan       lsgan_adversarial_loss criterion.py:90-103
+  split_frames  the discriminator's per-frame slices x[:, 3f:3f+3] (utils.py:116-118)
   weighted_sum  loss assembly utils.py:150-152
 """
 import ctypes
@@ -86,9 +88,11 @@ def new_act(shape, like):
     return buf if cp == c else buf[..., :c]
 
 
-def _grad_sink(p):
-    """(buffer to accumulate a parameter gradient into, value autograd should get)."""
-    if p is None or not p.requires_grad:
+def _grad_sink(p, need=True):
+    """(buffer to accumulate a parameter gradient into, value autograd should get).
+    `need`: ctx.needs_input_grad of the parameter (fixed at forward time, so a
+    parameter frozen during the forward — vae2.model.frozen — gets no gradient)."""
+    if p is None or not need or not p.requires_grad:
         return None, None
     mg = getattr(p, "main_grad", None)
     if mg is not None:
@@ -289,13 +293,13 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     return y
 
 
-def _conv_bwd(x, weight, bias, dy, spec, need_dx):
+def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
     """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b)."""
     s = stream_ptr()
     xp, xa = act_of(x)
     dyp, dya = act_of(dy)
-    wsink, wret = _grad_sink(weight)
-    bsink, bret = _grad_sink(bias)
+    wsink, wret = _grad_sink(weight, need_w)
+    bsink, bret = _grad_sink(bias, need_b)
     if wsink is not None or bsink is not None:
         if wsink is None:  # weight frozen but bias trained: still need a dW target
             wsink = torch.zeros_like(weight)
@@ -404,8 +408,8 @@ class _ConvBN(torch.autograd.Function):
         call("vae2_bn_relu_bwd_reduce", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
              ctypes.byref(ra), ptr(save), int(spec.relu), ptr(part), s)
         lsums = _empty((2 * cout,), r, torch.float64)
-        gsink, gret = _grad_sink(gamma)
-        bsink, bret = _grad_sink(beta)
+        gsink, gret = _grad_sink(gamma, ctx.needs_input_grad[3])
+        bsink, bret = _grad_sink(beta, ctx.needs_input_grad[4])
         call("vae2_bn_bwd_reduce_param_grads", ptr(part), rows, cout, ptr(lsums), ptr(gsink),
              ptr(bsink), s)
         gsums, _ = _all_reduce_sums(lsums, ctx.count, ctx.group)
@@ -427,7 +431,8 @@ class _ConvBN(torch.autograd.Function):
             else:  # (not reached by the blocks: conv1's backward runs after this one)
                 link.buf.add_(dres)
             dres = link.finish()
-        dx, wret, bret_conv = _conv_bwd(x, weight, bias, dr, spec, ctx.needs_input_grad[0])
+        dx, wret, bret_conv = _conv_bwd(x, weight, bias, dr, spec, ctx.needs_input_grad[0],
+                                        ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, wret, bret_conv, gret, bret, dres, None
 
 
@@ -452,7 +457,8 @@ class _Conv(torch.autograd.Function):
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         weight, bias = ctx.params
-        dx, wret, bret = _conv_bwd(x, weight, bias, as_act(dy), ctx.spec, ctx.needs_input_grad[0])
+        dx, wret, bret = _conv_bwd(x, weight, bias, as_act(dy), ctx.spec, ctx.needs_input_grad[0],
+                                   ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, wret, bret, None
 
 
@@ -750,6 +756,87 @@ class _L1(torch.autograd.Function):
 def l1(pred, target, scale, flat=False):
     """scale * sum |pred - target| (NHWC views, or any dense layout with flat=True)."""
     return _L1.apply(pred, target, float(scale), flat)
+
+
+class _LSGAN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target, scale, flat):
+        if flat:
+            x, xa = _flat_act(x)
+            xp = ptr(x)
+        else:
+            xp, xa = act_of(x)
+        ws = _empty((_lib.load().vae2_reduce_ws_size(xa.n * xa.h * xa.w * xa.c),), x)
+        out = _empty((), x)
+        call("vae2_lsgan_fwd", xp, ctypes.byref(xa), target, scale, ptr(ws), ptr(out),
+             stream_ptr())
+        ctx.target, ctx.scale, ctx.flat = target, scale, flat
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x,) = ctx.saved_tensors
+        gout = gout.contiguous()
+        if ctx.flat:
+            _, xa = _flat_act(x)
+            dx = torch.empty_like(x)
+            xp, dxp, dxa = ptr(x), ptr(dx), xa
+        else:
+            xp, xa = act_of(x)
+            dx = new_act(tuple(x.shape), x)
+            dxp, dxa = act_of(dx)
+        call("vae2_lsgan_bwd", xp, ctypes.byref(xa), ctx.target, ptr(gout), ctx.scale, dxp,
+             ctypes.byref(dxa), 0.0, stream_ptr())
+        return dx, None, None, None
+
+
+def lsgan(sample, real, scale, flat=False):
+    """scale * sum (sample - (1 if real else 0))^2  (LSGAN, criterion.py:90-103)."""
+    return _LSGAN.apply(sample, 1.0 if real else 0.0, float(scale), flat)
+
+
+class _SplitFrames(torch.autograd.Function):
+    """x (N,H,W,C) -> nframes contiguous (N,H,W,3) maps x[..., 3f:3f+3]; the backward
+    writes every frame gradient into one dx (no autograd slice/add kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, nframes):
+        n, h, w, c = x.shape
+        if 3 * nframes > c:
+            raise ValueError(f"{nframes} RGB frames do not fit {c} channels (the reference's "
+                             "frame loop needs CLIP_LENGTH 3 or more, utils.py:116)")
+        s = stream_ptr()
+        outs = []
+        for f in range(nframes):
+            o = new_act((n, h, w, 3), x)
+            sp, sa = act_of(x[..., 3 * f:3 * f + 3])
+            op, oa = act_of(o)
+            call("vae2_copy_act", sp, ctypes.byref(sa), op, ctypes.byref(oa), 0.0, s)
+            outs.append(o)
+        ctx.shape = tuple(x.shape)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        n, h, w, c = ctx.shape
+        ref = next(g for g in gs if g is not None)
+        dx = new_act(ctx.shape, ref)
+        if 3 * len(gs) < c or any(g is None for g in gs):
+            dx.zero_()
+        s = stream_ptr()
+        for f, g in enumerate(gs):
+            if g is None:
+                continue
+            g = as_act(g)
+            gp, ga = act_of(g)
+            dp_, da = act_of(dx[..., 3 * f:3 * f + 3])
+            call("vae2_copy_act", gp, ctypes.byref(ga), dp_, ctypes.byref(da), 0.0, s)
+        return dx, None
+
+
+def split_frames(x, nframes):
+    return _SplitFrames.apply(x, int(nframes))
 
 
 class _ReparamKL(torch.autograd.Function):

@@ -2,8 +2,8 @@
 
   adversarial_train   per-epoch loop (function.py:443-553): H2D, ELBO forward,
                       loss reduce, zero_grad / backward / RCCL grad all-reduce /
-                      Adam, meters, PRINT_FREQ logging.  The discriminator step
-                      runs only when the GAN path exists.
+                      Adam, the discriminator step (FullModel_D, Adam on the D
+                      parameters), meters, PRINT_FREQ logging.
   SyntheticClips      Cityscapes-shaped clips (3 segments x CLIP_LENGTH RGB frames
                       stacked on channels, cityscapes.py:311-326) for
                       benchmarking and CI; the zip/PNG dataset is next-2.
@@ -109,6 +109,9 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
                       seeds=None):
     """One epoch of the VAE² ELBO step (function.py:443-553)."""
     model_encdec.train()
+    if model_D is not None:
+        model_D.train()
+    fm = getattr(model_encdec, "module", model_encdec)
     batch_time = AverageMeter()
     ave_loss_D = AverageMeter()
     ave_loss_encdec = AverageMeter()
@@ -136,9 +139,20 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
         vdist.allreduce_grads(flats)
         optimizer_encdec.step()
         if model_D is not None and (not is_baseline or baseline_mode == "VAE_GAN"):
-            raise NotImplementedError("discriminator step: SURVEY.md §8f next-1")
-        reduced_loss_D = torch.zeros(1)
-        loss_D_sequence = loss_D_frame = 0.0
+            # D step (function.py:503-512): real x2t (x3t in baseline) vs detached x2t_hat
+            losses_D = model_D(x2t=x2t if not is_baseline else x3t,
+                               x2t_predict=x2t_predict.detach())
+            loss_D, loss_D_sequence, loss_D_frame = losses_D
+            reduced_loss_D = vdist.reduce_tensor(loss_D.detach().clone())
+            optimizer_D.zero_grad()
+            loss_D.backward()
+            vdist.allreduce_grads(optimizer_D.flats)
+            optimizer_D.step()
+        else:
+            reduced_loss_D = torch.zeros(1)
+            loss_D_sequence = loss_D_frame = 0.0
+        if getattr(fm, "defer_checks", False) and i_iter % config.PRINT_FREQ == 0:
+            fm.check_anomalies()  # deferred NaN/Inf flag (utils.py:63-65), one sync
         batch_time.update(time.time() - tic)
         tic = time.time()
         ave_loss_D.update(float(reduced_loss_D.item()))
@@ -152,13 +166,13 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
                    "loss_xt_recon: {:.6f}, loss_x2t_recon: {:.6f}, loss_x3t_recon: {:.6f}，"
                    "loss_z_KL: {:.6f}, loss_x2t_gan_sequence: {:.6f}, loss_x2t_gan_frame: {:.6f}"
                    ).format(epoch, num_epoch, i_iter, epoch_iters, batch_time.average(), base_lr,
-                            print_loss_D, loss_D_sequence, loss_D_frame, print_loss_encdec,
+                            print_loss_D, f(loss_D_sequence), f(loss_D_frame), print_loss_encdec,
                             f(loss_xt_recon), f(loss_x2t_recon), f(loss_x3t_recon), f(loss_z_KL),
                             f(loss_x2t_gan_sequence), f(loss_x2t_gan_frame))
             logging.info(msg)
             for tag, val in (("train_loss_D", print_loss_D),
-                             ("train_loss_D_sequence", loss_D_sequence),
-                             ("train_loss_D_frame", loss_D_frame),
+                             ("train_loss_D_sequence", f(loss_D_sequence)),
+                             ("train_loss_D_frame", f(loss_D_frame)),
                              ("train_loss_encdec", print_loss_encdec),
                              ("train_loss_xt_recon", f(loss_xt_recon)),
                              ("train_loss_x2_recon", f(loss_x2t_recon)),
