@@ -4,26 +4,33 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2], the metric's config): HRNet-W18-small-v2
-encoder + two decoders + posterior net, 128x256 clips of 3 x CLIP_LENGTH=3 = 9
-frames, 8 clips per GPU (weak scaling; 64 clips at 8 GPUs), fp32, random-init
-weights (seed 0, the reference's init), synthetic Gaussian clips resident in HBM.
-One step = posterior net + reparameterisation + encoder + 2 decoders forward,
-L1 x3 + KL, backward, RCCL gradient all-reduce (N > 1, SyncBN statistics),
-Adam.  frames/s = clips * 9 / step time, whole job.  At N=1 the step is
-captured once as a HIP graph (vae2.graph.StepGraph: same kernels, one launch,
-bit-identical to eager steps — tests/test_graph_gpu.py) and replayed; the noise
-is drawn on the device inside the step so every replay samples fresh noise.
+Workload (BASELINE.json configs[2], the metric's config): the shipped experiment
+YAML (vae-2_amd/experiments/vae2_w18_small_v2_128x256.yaml) through the drop-in
+surface — lib/config, models.enc_hrnet factories, utils.utils.FullModel_encdec,
+core.criterion — HRNet-W18-small-v2 encoder + two decoders + posterior net,
+128x256 clips of 3 x CLIP_LENGTH=3 = 9 frames, 8 clips per GPU (weak scaling; 64
+clips at 8 GPUs), fp32, random-init weights (seed 0, the reference's init),
+synthetic Gaussian clips resident in HBM.  One step = posterior net +
+reparameterisation + encoder + 2 decoders forward, L1 x3 + KL, backward, RCCL
+gradient all-reduce (N > 1, SyncBN statistics), Adam.  frames/s = clips * 9 /
+step time, whole job.  At N=1 the step is captured once as a HIP graph
+(vae2.graph.StepGraph: same kernels, one launch, bit-identical to eager steps —
+tests/test_graph_gpu.py) and replayed; the noise is drawn on the device inside the
+step so every replay samples fresh noise.
 
 Printed JSON also carries:
-  roofline      the dominant conv kernel (the igemm instantiation that runs the
-                64->64 3x3 full-resolution convs), timed live with HIP events
-                around its launches during --roofline-steps extra steps that follow
-                the timed region (each timed launch isolated from the side streams,
-                so the span is the kernel's own execution, as rocprof measures it);
-                achieved = algorithmic FLOPs per launch / average launch time,
-                against the fp32 matrix peak (157.3 TFLOP/s, MI355X_MICROARCH.md);
-                traffic = HBM bytes per launch from the committed PMC measurement.
+  roofline      the dominant kernel by time (one instantiation, as rocprofv3 names
+                it), timed live with HIP events around its launches during
+                --roofline-steps eager steps after the timed region (every C-ABI
+                call isolated from the side streams, so the span is the kernel's
+                own execution); achieved = algorithmic FLOPs (convs) or bytes per
+                launch / average launch time; traffic = HBM bytes per launch from the
+                committed PMC measurement (profiles/*_pmc_traffic.json) when present;
+                step_frac = the step's algorithmic conv FLOPs / step time / fp32 peak
+  families      the same profiled steps per kernel family (conv fwd / dgrad /
+                wgrad, BatchNorm, heads, fuse/resample, ...): ms per step, launches,
+                algorithmic GFLOP or GB and the rate against the roofline; the full
+                per-kernel and per-layer-shape tables go to --profile-json
   cpu_baseline  the CPU oracle (oracle/ref_cpu.py, the reference's ops on CPU)
                 timed on this host's cores, rank 0 at N=1 only, on a bounded sample.
 """
@@ -34,14 +41,18 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-for _p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+PKG = os.path.join(ROOT, "vae-2_amd")
+for _p in (ROOT, PKG, os.path.join(PKG, "lib")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-FP32_MFMA_PEAK_TF = 157.3
+YAML = os.path.join(PKG, "experiments", "vae2_w18_small_v2_128x256.yaml")
+METRIC = "training frames/sec on 128x256 8-frame Cityscapes clips, 1/2/4/8 MI355X"
+# ELBO FLOPs per clip at 128x256 (FlopCounterMode over the reference)
+REF_GFLOP_PER_CLIP = {(128, 256): 538.1, (64, 64): 67.27, (32, 32): 16.82, (256, 512): 2152.0}
 
 
 def parse():
@@ -49,19 +60,49 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
-    ap.add_argument("--height", type=int, default=128)
-    ap.add_argument("--width", type=int, default=256)
-    ap.add_argument("--clip-length", type=int, default=3)
-    ap.add_argument("--arch", default="w18")
+    ap.add_argument("--cfg", default=YAML)
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU (YAML: 8)")
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--clip-length", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
+    ap.add_argument("--profile-json", default=None,
+                    help="write the live per-family / per-kernel / per-shape tables here")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto: at N=1)")
     return ap.parse_args()
+
+
+def load_config(args):
+    """The experiment YAML through the drop-in config surface, plus shape overrides."""
+    from config import config
+    config.defrost()
+    config.merge_from_file(args.cfg)
+    opts = []
+    if args.batch is not None:
+        opts += ["TRAIN.BATCH_SIZE_PER_GPU", str(args.batch)]
+    if args.height is not None or args.width is not None:
+        w, h = config.TRAIN.IMAGE_SIZE
+        opts += ["TRAIN.IMAGE_SIZE", f"[{args.width or w}, {args.height or h}]"]
+    if args.clip_length is not None:  # 3 segments of L frames (SURVEY §8d)
+        opts += ["TRAIN.CLIP_LENGTH", str(args.clip_length),
+                 "DATASET.NUM_CLASSES", str(args.clip_length)]
+    config.merge_from_list(opts)
+    config.freeze()
+    return config
+
+
+def build_models(config):
+    """train.py's construction order (train.py:79-82) through the lib/ factories."""
+    import models
+    torch.manual_seed(0)
+    ed = models.enc_hrnet.get_encdec_model(config)
+    ez = models.enc_hrnet.get_encz_model(config)
+    return ed, ez
 
 
 def pmc_traffic(kernel):
@@ -81,16 +122,30 @@ def pmc_traffic(kernel):
     return best
 
 
-def cpu_baseline(args):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, config, gpu_batch):
     """Oracle ELBO step (fwd + bwd + torch Adam) on the host CPU, bounded sample."""
-    from helpers import build, make_cfg
     from oracle import ref_cpu
-    cores = min(16, len(os.sched_getaffinity(0)))
+    aff = len(os.sched_getaffinity(0))
+    # the box's CPU share for one GPU is OMP_NUM_THREADS (16); never more than affinity
+    cores = min(aff, int(os.environ.get("OMP_NUM_THREADS", aff)))
     torch.set_num_threads(cores)
-    L, H, W, B = args.clip_length, args.height, args.width, args.cpu_batch
-    ed, ez = build(make_cfg(args.arch, L=L, hw=(H, W)))
+    L = config.TRAIN.CLIP_LENGTH
+    W, H = config.TRAIN.IMAGE_SIZE
+    B = args.cpu_batch
+    ed, ez = build_models(config)
     params = list(ez.parameters()) + list(ed.parameters())
-    opt = torch.optim.Adam(params, lr=1e-4)
+    opt = torch.optim.Adam(params, lr=config.TRAIN.LR)
     g = torch.Generator().manual_seed(1)
     xs = [torch.randn(B, 3 * L, H, W, generator=g) for _ in range(3)]
 
@@ -109,9 +164,12 @@ def cpu_baseline(args):
     dt = (time.perf_counter() - t0) / args.cpu_steps
     return {"value": round(B * 3 * L / dt, 3), "unit": "frames/s", "cores": cores,
             "kind": "port",
-            "sample": f"oracle/ref_cpu.py ELBO step fwd+bwd+Adam, {args.arch} {H}x{W}, "
-                      f"{B} clips x {3 * L} frames, fp32, 1 warm-up + {args.cpu_steps} timed "
-                      f"steps ({dt:.2f} s/step), torch CPU threads={cores}"}
+            "sample": f"oracle/ref_cpu.py ELBO step fwd+bwd+torch Adam (the reference's ATen "
+                      f"ops), HRNet-W18-small-v2 {H}x{W}, {B} clips x {3 * L} frames per step "
+                      f"(the GPU runs {gpu_batch} clips/step; frames/s is per-frame, so the "
+                      f"sample size only bounds the run time), fp32, 1 warm-up + "
+                      f"{args.cpu_steps} timed steps ({dt:.2f} s/step), torch threads={cores} "
+                      f"of {aff} in the affinity mask, CPU: {cpu_model()}"}
 
 
 def main():
@@ -125,19 +183,24 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from helpers import build, make_cfg
+    from core.criterion import KLLoss, L1Loss
+    from utils.utils import FullModel_encdec
     from vae2 import dist as vdist
     from vae2 import prof
-    from vae2.model import FullModel_encdec
     from vae2.optim import FusedAdam
-    vdist.set_sync_bn(True)
+    config = load_config(args)
+    vdist.set_sync_bn(config.MI355X.SYNC_BN)
 
-    L, H, W, B = args.clip_length, args.height, args.width, args.batch
-    ed, ez = build(make_cfg(args.arch, L=L, hw=(H, W)))
-    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(dev)
+    L = config.TRAIN.CLIP_LENGTH
+    W, H = config.TRAIN.IMAGE_SIZE
+    B = config.TRAIN.BATCH_SIZE_PER_GPU
+    ed, ez = build_models(config)
+    fm = FullModel_encdec(ez, ed, None, None, L1Loss(), KLLoss(), None,
+                          config.TRAIN.X1RECON_LAMBDA, config.TRAIN.X2RECON_LAMBDA,
+                          config.TRAIN.X3RECON_LAMBDA, config.TRAIN.GAN_LAMBDA).to(dev)
     fm.train()
     fm.defer_checks = True
-    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-4)
+    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=config.TRAIN.LR)
     if world > 1:
         for f in opt.flats:
             dist.broadcast(f.data, src=0)
@@ -181,16 +244,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     fm.check_anomalies()
-    last_loss = float(loss)
+    last_loss = float(loss.detach())
 
-    # ---- roofline phase: the same step, the dominant kernel's launches timed with
-    # HIP events on their stream, each launch isolated from the side streams ----
-    from vae2 import _lib
-    kname = prof.fwd_kernel_name(_lib.Act(B, H, W, 64, 64), (B, H, W, 64), 3, 1, 1)
-    timer = prof.KernelTimer(kname)
+    # ---- profiled phase: the same step eager, every C-ABI call timed with HIP events
+    # on its stream, isolated from the side streams ----
+    profiler = None
     if not args.no_roofline and args.roofline_steps > 0:
         torch.cuda.synchronize()
-        with timer:
+        with prof.StepProfiler() as profiler:
             for _ in range(args.roofline_steps):
                 eager_step()
         torch.cuda.synchronize()
@@ -200,38 +261,48 @@ def main():
         ms = 1e3 * elapsed / args.steps
         frames = world * B * 3 * L * args.steps
         out = {
-            "metric": "training frames/sec on 128x256 8-frame Cityscapes clips, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (Gaussian Cityscapes-shaped clips resident in HBM; random-init "
                     "weights, reference init seed 0)",
             "config": {"workload": f"VAE2 ELBO step (encz + encoder + 2 decoders fwd/bwd + "
-                                   f"Adam), HRNet-{args.arch}-small-v2, {H}x{W}, "
-                                   f"{B} clips/GPU x {3 * L} frames (CLIP_LENGTH={L})",
+                                   f"Adam), HRNet-W18-small-v2, {H}x{W}, {B} clips/GPU x "
+                                   f"{3 * L} frames (CLIP_LENGTH={L})",
+                       "yaml": os.path.relpath(args.cfg, ROOT),
                        "global_batch": world * B, "frames_per_clip": 3 * L,
                        "image": [H, W], "parallelism": f"dp{world}",
-                       "sync_bn": world > 1,
+                       "sync_bn": world > 1 and config.MI355X.SYNC_BN,
                        "launch": "hip_graph" if use_graph else "eager"},
             "last_loss": last_loss,
         }
-        summ = timer.summary() if not args.no_roofline else None
-        if summ:
-            tr = pmc_traffic(kname)
-            out["roofline"] = {"bound": "mfma", "kernel": kname,
-                               "achieved": round(summ["tflops"], 3), "peak": FP32_MFMA_PEAK_TF,
-                               "unit": "TFLOP/s",
-                               "frac": round(summ["tflops"] / FP32_MFMA_PEAK_TF, 4),
-                               "traffic": round(tr["hbm_bytes_per_launch"]) if tr else None,
-                               "traffic_unit": "bytes/launch (PMC)",
-                               "avg_launch_us": round(summ["avg_us"], 2),
-                               "flops_per_launch": summ["flops_per_launch"],
-                               "algorithmic_bytes_per_launch": summ["bytes_per_launch"],
-                               "launches": summ["launches"],
-                               "measured": f"{args.roofline_steps} steps after the timed region, "
-                                           "launches isolated from side streams (eager)"}
+        if profiler is not None:
+            n = args.roofline_steps
+            summ = profiler.summary(n)
+            dom = profiler.dominant(n)
+            conv_gf = sum(r.get("gflop_per_step", 0.0) for r in summ["families"])
+            ref_gf = REF_GFLOP_PER_CLIP.get((H, W))
+            roof = dict(dom)
+            tr = pmc_traffic(dom["kernel"])
+            roof["traffic"] = round(tr["hbm_bytes_per_launch"]) if tr else None
+            roof["traffic_unit"] = "HBM bytes/launch (PMC, profiles/)"
+            roof["step_frac"] = round(conv_gf / ms / prof.FP32_MFMA_PEAK_TF, 4)
+            roof["step_gflop"] = round(conv_gf, 1)
+            if ref_gf is not None and L == 3:
+                roof["step_frac_ref_flops"] = round(
+                    B * ref_gf / ms / prof.FP32_MFMA_PEAK_TF, 4)
+            roof["measured"] = (f"{n} eager steps after the timed region, every C-ABI call "
+                                "timed with HIP events on its stream, isolated from side "
+                                "streams")
+            out["roofline"] = roof
+            out["families"] = {r["name"]: {k: r[k] for k in r if k != "name"}
+                               for r in summ["families"]}
+            if args.profile_json:
+                with open(args.profile_json, "w") as f:
+                    json.dump(summ, f, indent=1)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+            out["cpu_baseline"] = cpu_baseline(args, config, B)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -32,10 +32,18 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 3
+#define VAE2_ABI_VERSION 4
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
+
+/* Kernel launch log for profilers (bench.py's live per-kernel table): with logging
+ * enabled every kernel the calling thread launches is recorded; _read returns how
+ * many were launched since the last read and writes their names (as rocprofv3 shows
+ * them, without "vae2::" and the parameter list, ';'-separated) into buf.  Enabling
+ * or disabling clears the log.                                                    */
+int vae2_kernel_log(int enable);
+int64_t vae2_kernel_log_read(char* buf, int64_t len);
 
 /* ---------------------------------------------------------------- conv ---- */
 
@@ -191,6 +199,53 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
                            const float* gamma, const double* sums, double count,
                            int relu, float* dx, const vae2_act* dxd,
                            float* dres, const vae2_act* dresd, void* stream);
+
+/* Multi-layer BatchNorm launches: the independent BN layers of one HRNet depth level
+ * (a HighResolutionModule's branches run in lockstep, its fuse convs, transition
+ * units) share each launch instead of one launch per layer (~3x fewer BN launches),
+ * and with SyncBN their statistics cross ranks in one exchange.  Same math as the
+ * single-layer calls above.  Layer tensors: 16-byte aligned NHWC, pixel stride % 4
+ * == 0, C <= 1024.  Any n (split into launches of 6 layers).                       */
+typedef struct vae2_bn_layer {
+  const float* x; vae2_act xd;    /* pre-BN activation (the conv output)               */
+  const float* a; vae2_act ad;    /* forward: residual, backward: y for the ReLU mask;  */
+                                  /* NULL: none / mask recomputed from x               */
+  float* o; vae2_act od;          /* forward: y; backward: dx                          */
+  const float* dy; vae2_act dyd;  /* backward                                          */
+  float* dres; vae2_act dresd;    /* backward: residual gradient (= masked dy) or NULL  */
+  const float* save;              /* [4][c]: mean, invstd, scale, shift                 */
+  const float* gamma;             /* backward apply (NULL: 1)                            */
+  float* partials;                /* backward reduce: [2][vae2_bn_partial_rows(xd)][c]  */
+  const double* sums;             /* backward apply: (sum g, sum g*xhat) [2][c]         */
+  const double* countp;           /* device element count per channel (SyncBN: summed  */
+  double count;                   /* over ranks), or NULL to use `count`               */
+  int relu;
+} vae2_bn_layer;
+/* y = relu?(fma(x, scale, shift) + a) per layer (vae2_bn_apply).                 */
+int vae2_bn_multi_apply(int n, const vae2_bn_layer* layers, void* stream);
+/* partials of (sum g, sum g*xhat) per layer (vae2_bn_relu_bwd_reduce).            */
+int vae2_bn_multi_bwd_reduce(int n, const vae2_bn_layer* layers, void* stream);
+/* dx (and dres) per layer (vae2_bn_relu_bwd_apply).                              */
+int vae2_bn_multi_bwd_apply(int n, const vae2_bn_layer* layers, void* stream);
+
+typedef struct vae2_bn_fin {
+  const float* partials; int64_t rows; int64_t c;  /* [2][rows][c] fp32 partial rows   */
+  double* sums;                   /* [2][c] out (mode 2 / finalize: in)                 */
+  const double* countp;           /* device count, or NULL to use `count`               */
+  double count;
+  const float* gamma; const float* beta;
+  float* running_mean; float* running_var; int64_t* num_batches_tracked;  /* or NULL  */
+  float momentum, eps;
+  float* save;                    /* [4][c] out (mode 0 / finalize)                     */
+  float* dgamma; float* dbeta;    /* mode 1: += (sum g*xhat, sum g), or NULL            */
+} vae2_bn_fin;
+/* Per layer, partial rows -> sums in double (fixed order), then mode 0: finalize
+ * (save + running statistics, vae2_bn_reduce_finalize), mode 1: backward parameter
+ * gradients (vae2_bn_bwd_reduce_param_grads), mode 2: sums only (SyncBN: exchange,
+ * then vae2_bn_multi_finalize).                                                    */
+int vae2_bn_multi_reduce(int n, const vae2_bn_fin* fins, int mode, void* stream);
+/* save + running statistics from sums (vae2_bn_finalize).                         */
+int vae2_bn_multi_finalize(int n, const vae2_bn_fin* fins, void* stream);
 
 /* ---------------------------------------------------------- head output ---- */
 /* 1x1 conv of a channel-concatenation of bilinearly upsampled maps, computed per

@@ -520,6 +520,267 @@ __global__ __launch_bounds__(256) void colsum_to_float_kernel(
   }
 }
 
+// ------------------------------------------------ multi-layer launches ----
+// The independent BatchNorm layers of one HRNet depth level (the branches of a
+// HighResolutionModule run in lockstep, the fuse convs of a module, the units of the
+// transitions) share each launch: blocks are partitioned between the layers by
+// prefix (blk0), each block runs the single-layer body on its own layer.  Up to
+// kBnMaxLayers layers per launch (host splits larger groups).  Quad path only.
+constexpr int kBnMaxLayers = 6;
+
+struct BnLayer {
+  const float* x;       // pre-BN activation r (the conv output)
+  const float* a;       // forward: residual (or null); backward: y for the ReLU mask (or null)
+  float* o;             // forward: y; backward: dx
+  const float* dy;      // backward
+  float* dres;          // backward: residual gradient (or null)
+  float* part;          // backward reduce: partial rows [2][nblk][C]
+  const float* save;    // mean, invstd, scale, shift
+  const float* gamma;
+  const double* sums;   // backward apply: global (sum g, sum g*xhat)
+  const double* countp; // device count (SyncBN: all-reduced) or null -> count
+  double count;
+  int64_t P, ppb;
+  int C, x_ps, a_ps, o_ps, dy_ps, dres_ps, relu, rows, blk0;
+};
+
+struct BnMulti {
+  BnLayer L[kBnMaxLayers];
+  int n;
+};
+
+__device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
+  int i = 0;
+  while (i + 1 < m.n && b >= m.L[i + 1].blk0) ++i;
+  return i;
+}
+
+__device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= L.rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
+  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  f4 v[kApplyU], rv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * L.rows;
+    if (p < L.P) {
+      v[u] = ld4(L.x + p * L.x_ps + c);
+      if (L.a) rv[u] = ld4(L.a + p * L.a_ps + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * L.rows;
+    if (p >= L.P) break;
+    f4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float t = __builtin_fmaf(v[u][k], sc[k], sh[k]);
+      if (L.a) t += rv[u][k];
+      o[k] = (L.relu && t < 0.f) ? 0.f : t;  // NaN propagates (torch.relu)
+    }
+    st4(L.o + p * L.o_ps + c, o, c, C);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_multi_kernel(BnMulti m) {
+  const int i = bn_layer_of(m, blockIdx.x);
+  bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
+}
+
+// Backward partials (sum g, sum g*xhat) of one layer's pixel range blk*ppb ...
+__device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, int nblk,
+                                                   float* red0, float* red1) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  const int64_t p0 = blk * L.ppb;
+  int64_t p1 = p0 + L.ppb;
+  if (p1 > L.P) p1 = L.P;
+  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const float* y = L.relu ? L.a : nullptr;
+  if (tid < L.rows * c4) {
+    const f4 mean = chan4(L.save, c, C), invstd = chan4(L.save + C, c, C);
+    const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
+    for (int64_t p = p0 + r; p < p1; p += L.rows) {
+      const f4 xa = ld4(L.x + p * L.x_ps + c);
+      f4 ga = ld4(L.dy + p * L.dy_ps + c);
+      f4 ya;
+      if (y) ya = ld4(y + p * L.a_ps + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (L.relu && !((y ? ya[k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f)) ga[k] = 0.f;
+        s0[k] += ga[k];
+        s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red0[r * 4 * c4 + c + k] = s0[k];
+      red1[r * 4 * c4 + c + k] = s1[k];
+    }
+  }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < L.rows; ++i) {
+      a += red0[i * 4 * c4 + ch];
+      b += red1[i * 4 * c4 + ch];
+    }
+    L.part[(int64_t)blk * C + ch] = a;
+    L.part[((int64_t)nblk + blk) * C + ch] = b;
+  }
+}
+
+// nblk of layer i = blk0[i+1] - blk0[i] (the last: gridDim.x - blk0)
+__global__ __launch_bounds__(256) void bn_bwd_reduce_multi_kernel(BnMulti m) {
+  __shared__ float red[2][256 * 4];
+  const int i = bn_layer_of(m, blockIdx.x);
+  const int nblk = (i + 1 < m.n ? m.L[i + 1].blk0 : (int)gridDim.x) - m.L[i].blk0;
+  bn_bwd_reduce_body(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
+}
+
+__device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= L.rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const double count = L.countp ? *L.countp : L.count;
+  const float inv_n = (float)(1.0 / count);
+  const float* y = L.relu ? L.a : nullptr;
+  f4 mean, invstd, sc, sh, mg, mgx, k4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = c + k < C ? c + k : C - 1;
+    mean[k] = L.save[ch];
+    invstd[k] = L.save[C + ch];
+    sc[k] = L.save[2 * C + ch];
+    sh[k] = L.save[3 * C + ch];
+    mg[k] = (float)L.sums[ch] * inv_n;
+    mgx[k] = (float)L.sums[C + ch] * inv_n;
+    k4[k] = (L.gamma ? L.gamma[ch] : 1.f) * invstd[k];
+  }
+  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * L.rows;
+    if (p < L.P) {
+      gv[u] = ld4(L.dy + p * L.dy_ps + c);
+      xv[u] = ld4(L.x + p * L.x_ps + c);
+      if (y) yv[u] = ld4(y + p * L.a_ps + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const int64_t p = pb + u * L.rows;
+    if (p >= L.P) break;
+    f4 g = gv[u], o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (L.relu && !((y ? yv[u][k] : __builtin_fmaf(xv[u][k], sc[k], sh[k])) > 0.f)) g[k] = 0.f;
+      const float xh = (xv[u][k] - mean[k]) * invstd[k];
+      o[k] = k4[k] * (g[k] - mg[k] - xh * mgx[k]);
+    }
+    if (L.dres) st4(L.dres + p * L.dres_ps + c, g, c, C);
+    st4(L.o + p * L.o_ps + c, o, c, C);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
+  const int i = bn_layer_of(m, blockIdx.x);
+  bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
+}
+
+// One block per (layer, channel): reduce the layer's partial rows in double (fixed
+// order), then MODE 0: finalize (+ running statistics); MODE 1: sums + dgamma/dbeta
+// (backward); MODE 2: sums only (SyncBN, exchanged before vae2_bn_multi_finalize).
+struct FinLayer {
+  const float* part;
+  double* sums;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float* save;
+  float* dgamma;
+  float* dbeta;
+  const double* countp;
+  double count;
+  int64_t rows;
+  float momentum, eps;
+  int C, blk0;
+};
+
+struct FinMulti {
+  FinLayer L[kBnMaxLayers];
+  int n;
+};
+
+__device__ __forceinline__ void bn_finalize_channel(const FinLayer& L, int c, double s0,
+                                                    double s1) {
+  const double count = L.countp ? *L.countp : L.count;
+  if (c == 0 && L.nbt) L.nbt[0] += 1;
+  const double mean = s0 / count;
+  double var = s1 / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)L.eps);
+  const float gm = L.gamma ? L.gamma[c] : 1.f;
+  const float bt = L.beta ? L.beta[c] : 0.f;
+  L.save[c] = (float)mean;
+  L.save[L.C + c] = (float)invstd;
+  L.save[2 * L.C + c] = (float)(gm * invstd);
+  L.save[3 * L.C + c] = (float)(bt - mean * (gm * invstd));
+  if (L.rmean) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    L.rmean[c] = (float)((1.0 - L.momentum) * L.rmean[c] + L.momentum * mean);
+    L.rvar[c] = (float)((1.0 - L.momentum) * L.rvar[c] + L.momentum * unbiased);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void reduce_then_multi_kernel(FinMulti m) {
+  __shared__ double red[2][4];
+  int i = 0;
+  while (i + 1 < m.n && (int)blockIdx.x >= m.L[i + 1].blk0) ++i;
+  const FinLayer& L = m.L[i];
+  const int c = blockIdx.x - L.blk0;
+  const int tid = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int64_t r = tid; r < L.rows; r += 256) {
+    a += (double)L.part[r * L.C + c];
+    b += (double)L.part[(L.rows + r) * L.C + c];
+  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = a;
+    red[1][tid >> 6] = b;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  const double s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const double s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  L.sums[c] = s0;
+  L.sums[L.C + c] = s1;
+  if (MODE == 1) {
+    if (L.dgamma) L.dgamma[c] += (float)s1;
+    if (L.dbeta) L.dbeta[c] += (float)s0;
+  } else if (MODE == 0) {
+    bn_finalize_channel(L, c, s0, s1);
+  }
+}
+
+// From (all-reduced) sums: one block per layer, threads over channels.
+__global__ __launch_bounds__(256) void bn_finalize_multi_kernel(FinMulti m) {
+  const FinLayer& L = m.L[blockIdx.x];
+  for (int c = threadIdx.x; c < L.C; c += 256) bn_finalize_channel(L, c, L.sums[c], L.sums[L.C + c]);
+}
+
 static bool v4_ok(const void* p, int64_t ps) {
   return ((uintptr_t)p % 16 == 0) && (ps % 4 == 0);
 }
@@ -528,7 +789,7 @@ static bool quad_ok(int64_t c) { return (c + 3) / 4 <= 256; }
 
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream) {
-  hipLaunchKernelGGL(colsum_to_float_kernel, dim3((unsigned)c), dim3(256), 0,
+  VAE2_LAUNCH(colsum_to_float_kernel, dim3((unsigned)c), dim3(256), 0,
                      as_stream(stream), partials, rows, c, dbias, accumulate);
   return check_launch("bias_grad_from_partials");
 }
@@ -552,13 +813,13 @@ int vae2_bn_stats(const float* x, const vae2_act* xd, float* partials,
   int64_t ppb = pix_per_block(P);
   Act a = to_act(xd);
   if (quad_ok(xd->c) && v4_ok(x, xd->ps)) {
-    hipLaunchKernelGGL((chan_partials_q_kernel<0>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
+    VAE2_LAUNCH((chan_partials_q_kernel<0>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
                        0, as_stream(stream), x, a, (const float*)nullptr, a,
                        (const float*)nullptr, a, (const float*)nullptr, 0, ppb,
                        quad_rows(xd->c), partials);
     return check_launch(fn);
   }
-  hipLaunchKernelGGL((chan_partials_kernel<0>), dim3((unsigned)ceil_div(P, ppb)),
+  VAE2_LAUNCH((chan_partials_kernel<0>), dim3((unsigned)ceil_div(P, ppb)),
                      dim3(256), 0, as_stream(stream), x, a, (const float*)nullptr, a,
                      (const float*)nullptr, a, (const float*)nullptr, 0, ppb, partials);
   return check_launch(fn);
@@ -568,7 +829,7 @@ int vae2_bn_partials_reduce(const float* partials, int64_t rows, int64_t c,
                             double* sums, int accumulate, void* stream) {
   const char* fn = "vae2_bn_partials_reduce";
   VAE2_REQUIRE(partials && sums && rows > 0 && c > 0, fn, "bad arguments");
-  hipLaunchKernelGGL(partials_reduce_kernel, dim3((unsigned)c), dim3(256), 0,
+  VAE2_LAUNCH(partials_reduce_kernel, dim3((unsigned)c), dim3(256), 0,
                      as_stream(stream), partials, rows, c, sums, accumulate);
   return check_launch(fn);
 }
@@ -581,7 +842,7 @@ int vae2_bn_finalize(const double* sums, double count, const float* gamma,
   VAE2_REQUIRE(sums && save && c > 0 && count > 0, fn, "bad arguments");
   VAE2_REQUIRE((running_mean == nullptr) == (running_var == nullptr), fn,
                "running_mean and running_var must both be set or both be null");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
+  VAE2_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
                      as_stream(stream), sums, count, gamma, beta, running_mean,
                      running_var, num_batches_tracked, momentum, eps, c, save);
   return check_launch(fn);
@@ -596,7 +857,7 @@ int vae2_bn_reduce_finalize(const float* partials, int64_t rows, int64_t c,
   VAE2_REQUIRE(partials && sums && save && rows > 0 && c > 0 && count > 0, fn, "bad arguments");
   VAE2_REQUIRE((running_mean == nullptr) == (running_var == nullptr), fn,
                "running_mean and running_var must both be set or both be null");
-  hipLaunchKernelGGL((reduce_then_kernel<0>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
+  VAE2_LAUNCH((reduce_then_kernel<0>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
                      partials, rows, c, sums, count, gamma, beta, running_mean, running_var,
                      num_batches_tracked, momentum, eps, save, (float*)nullptr, (float*)nullptr);
   return check_launch(fn);
@@ -606,7 +867,7 @@ int vae2_bn_bwd_reduce_param_grads(const float* partials, int64_t rows, int64_t 
                                    double* sums, float* dgamma, float* dbeta, void* stream) {
   const char* fn = "vae2_bn_bwd_reduce_param_grads";
   VAE2_REQUIRE(partials && sums && rows > 0 && c > 0, fn, "bad arguments");
-  hipLaunchKernelGGL((reduce_then_kernel<1>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
+  VAE2_LAUNCH((reduce_then_kernel<1>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
                      partials, rows, c, sums, 1.0, (const float*)nullptr, (const float*)nullptr,
                      (float*)nullptr, (float*)nullptr, (int64_t*)nullptr, 0.f, 0.f, (float*)nullptr,
                      dgamma, dbeta);
@@ -618,7 +879,7 @@ int vae2_bn_eval_coeffs(const float* gamma, const float* beta,
                         float eps, int64_t c, float* save, void* stream) {
   const char* fn = "vae2_bn_eval_coeffs";
   VAE2_REQUIRE(running_mean && running_var && save && c > 0, fn, "bad arguments");
-  hipLaunchKernelGGL(bn_eval_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
+  VAE2_LAUNCH(bn_eval_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
                      as_stream(stream), gamma, beta, running_mean, running_var, eps, c,
                      save);
   return check_launch(fn);
@@ -641,7 +902,7 @@ int vae2_bn_apply(const float* x, const vae2_act* xd, const float* save,
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
   if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(y, yd->ps) && (!res || v4_ok(res, rd->ps))) {
     const int rows = quad_rows(xd->c);
-    hipLaunchKernelGGL(bn_apply_q_kernel,
+    VAE2_LAUNCH(bn_apply_q_kernel,
                        dim3((unsigned)ceil_div(act_pixels(xd), (int64_t)rows * kApplyU)),
                        dim3(256), 0, as_stream(stream), x, to_act(xd), save, res, r, y,
                        to_act(yd), relu, rows);
@@ -650,11 +911,11 @@ int vae2_bn_apply(const float* x, const vae2_act* xd, const float* save,
   bool vec = (xd->c % 4 == 0) && v4_ok(x, xd->ps) && v4_ok(y, yd->ps) &&
              (!res || v4_ok(res, rd->ps)) && v4_ok(save, 4);
   if (vec) {
-    hipLaunchKernelGGL(bn_apply_kernel_v4, dim3(ew_blocks(total / 4)), dim3(256), 0,
+    VAE2_LAUNCH(bn_apply_kernel_v4, dim3(ew_blocks(total / 4)), dim3(256), 0,
                        as_stream(stream), x, to_act(xd), save, res, r, y, to_act(yd), relu,
                        FastDiv((uint32_t)(xd->c / 4)));
   } else {
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+    VAE2_LAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                        as_stream(stream), x, to_act(xd), save, res, r, y, to_act(yd), relu,
                        FastDiv((uint32_t)xd->c));
   }
@@ -673,12 +934,12 @@ int vae2_bn_relu_bwd_reduce(const float* dy, const vae2_act* dyd,
   Act ya = (relu && y) ? to_act(yd) : to_act(xd);
   if (!relu) y = nullptr;
   if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(dy, dyd->ps) && (!y || v4_ok(y, yd->ps))) {
-    hipLaunchKernelGGL((chan_partials_q_kernel<1>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
+    VAE2_LAUNCH((chan_partials_q_kernel<1>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
                        0, as_stream(stream), x, to_act(xd), dy, to_act(dyd), y, ya, save, relu,
                        ppb, quad_rows(xd->c), partials);
     return check_launch(fn);
   }
-  hipLaunchKernelGGL((chan_partials_kernel<1>), dim3((unsigned)ceil_div(P, ppb)),
+  VAE2_LAUNCH((chan_partials_kernel<1>), dim3((unsigned)ceil_div(P, ppb)),
                      dim3(256), 0, as_stream(stream), x, to_act(xd), dy, to_act(dyd), y,
                      ya, save, relu, ppb, partials);
   return check_launch(fn);
@@ -688,7 +949,7 @@ int vae2_bn_bwd_param_grads(const double* sums, int64_t c, float* dgamma,
                             float* dbeta, void* stream) {
   const char* fn = "vae2_bn_bwd_param_grads";
   VAE2_REQUIRE(sums && c > 0, fn, "bad arguments");
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
+  VAE2_LAUNCH(bn_param_grad_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
                      as_stream(stream), sums, c, dgamma, dbeta);
   return check_launch(fn);
 }
@@ -711,7 +972,7 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
   if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(dy, dyd->ps) && v4_ok(dx, dxd->ps) &&
       (!y || v4_ok(y, yd->ps)) && (!dres || v4_ok(dres, dresd->ps))) {
     const int rows = quad_rows(xd->c);
-    hipLaunchKernelGGL(bn_bwd_apply_q_kernel,
+    VAE2_LAUNCH(bn_bwd_apply_q_kernel,
                        dim3((unsigned)ceil_div(act_pixels(xd), (int64_t)rows * kApplyU)),
                        dim3(256), 0, as_stream(stream), dy, to_act(dyd), y, ya, x, to_act(xd),
                        save, gamma, sums, count, relu, dx, to_act(dxd), dres,
@@ -719,11 +980,154 @@ int vae2_bn_relu_bwd_apply(const float* dy, const vae2_act* dyd, const float* y,
     return check_launch(fn);
   }
   Act ra = dres ? to_act(dresd) : to_act(xd);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(bn_bwd_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), dy, to_act(dyd), y, ya, x, to_act(xd), save, gamma,
                      sums, count, relu, dx, to_act(dxd), dres, ra,
                      FastDiv((uint32_t)xd->c));
   return check_launch(fn);
+}
+
+// ------------------------------------------------- multi-layer launchers ----
+static bool bn_layer_quad_ok(const vae2_bn_layer& l, bool bwd) {
+  const vae2_act& x = l.xd;
+  if (!l.x || !l.o || !l.save || !act_ok(&x) || !quad_ok(x.c) || !v4_ok(l.x, x.ps)) return false;
+  if (!v4_ok(l.o, l.od.ps) || l.od.n != x.n || l.od.h != x.h || l.od.w != x.w || l.od.c != x.c)
+    return false;
+  if (l.a && (!v4_ok(l.a, l.ad.ps) || l.ad.n != x.n || l.ad.h != x.h || l.ad.w != x.w ||
+              l.ad.c < x.c))
+    return false;
+  if (bwd) {
+    if (!l.dy || !v4_ok(l.dy, l.dyd.ps) || l.dyd.n != x.n || l.dyd.h != x.h || l.dyd.w != x.w)
+      return false;
+    if (l.dres && (!v4_ok(l.dres, l.dresd.ps) || l.dresd.c != x.c)) return false;
+  }
+  return act_pixels(&x) * x.c < (int64_t(1) << 31);
+}
+
+// kind 0: forward apply, 1: backward reduce, 2: backward apply
+static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* stream,
+                           const char* fn) {
+  VAE2_REQUIRE(n >= 0 && (n == 0 || ls), fn, "bad arguments");
+  for (int i0 = 0; i0 < n; i0 += kBnMaxLayers) {
+    BnMulti m{};
+    m.n = n - i0 < kBnMaxLayers ? n - i0 : kBnMaxLayers;
+    int blocks = 0;
+    for (int j = 0; j < m.n; ++j) {
+      const vae2_bn_layer& l = ls[i0 + j];
+      VAE2_REQUIRE(bn_layer_quad_ok(l, kind != 0), fn,
+                   "layer tensors must be 16-byte aligned NHWC with pixel strides % 4 == 0, "
+                   "matching shapes, C <= 1024");
+      VAE2_REQUIRE(kind == 0 || (kind == 1 ? l.partials != nullptr : l.sums != nullptr), fn,
+                   "missing partials / sums");
+      VAE2_REQUIRE(kind != 2 || l.countp || l.count > 0, fn, "bad count");
+      BnLayer& L = m.L[j];
+      L.x = l.x; L.a = l.a; L.o = l.o; L.dy = l.dy; L.dres = l.dres; L.part = l.partials;
+      L.save = l.save; L.gamma = l.gamma; L.sums = l.sums; L.countp = l.countp;
+      L.count = l.count;
+      L.P = act_pixels(&l.xd);
+      L.C = (int)l.xd.c;
+      L.x_ps = (int)l.xd.ps; L.a_ps = (int)l.ad.ps; L.o_ps = (int)l.od.ps;
+      L.dy_ps = (int)l.dyd.ps; L.dres_ps = (int)l.dresd.ps;
+      L.relu = l.relu;
+      L.rows = quad_rows(l.xd.c);
+      L.blk0 = blocks;
+      if (kind == 1) {
+        L.ppb = pix_per_block(L.P);
+        blocks += (int)ceil_div(L.P, L.ppb);
+      } else {
+        blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU);
+      }
+    }
+    if (blocks == 0) continue;
+    hipStream_t st = as_stream(stream);
+    if (kind == 0)
+      VAE2_LAUNCH(bn_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else if (kind == 1)
+      VAE2_LAUNCH(bn_bwd_reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else
+      VAE2_LAUNCH(bn_bwd_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    const int rc = check_launch(fn);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int vae2_bn_multi_apply(int n, const vae2_bn_layer* layers, void* stream) {
+  return bn_multi_launch(n, layers, 0, stream, "vae2_bn_multi_apply");
+}
+
+int vae2_bn_multi_bwd_reduce(int n, const vae2_bn_layer* layers, void* stream) {
+  return bn_multi_launch(n, layers, 1, stream, "vae2_bn_multi_bwd_reduce");
+}
+
+int vae2_bn_multi_bwd_apply(int n, const vae2_bn_layer* layers, void* stream) {
+  return bn_multi_launch(n, layers, 2, stream, "vae2_bn_multi_bwd_apply");
+}
+
+static int bn_fin_pack(int n, const vae2_bn_fin* fs, int i0, FinMulti& m, int& blocks,
+                       bool per_channel, const char* fn) {
+  m = FinMulti{};
+  m.n = n - i0 < kBnMaxLayers ? n - i0 : kBnMaxLayers;
+  blocks = 0;
+  for (int j = 0; j < m.n; ++j) {
+    const vae2_bn_fin& f = fs[i0 + j];
+    VAE2_REQUIRE(f.sums && f.c > 0 && f.c <= (1 << 20), fn, "bad layer");
+    FinLayer& L = m.L[j];
+    L.part = f.partials; L.sums = f.sums; L.gamma = f.gamma; L.beta = f.beta;
+    L.rmean = f.running_mean; L.rvar = f.running_var; L.nbt = f.num_batches_tracked;
+    L.save = f.save; L.dgamma = f.dgamma; L.dbeta = f.dbeta; L.countp = f.countp;
+    L.count = f.count; L.rows = f.rows; L.momentum = f.momentum; L.eps = f.eps;
+    L.C = (int)f.c;
+    L.blk0 = blocks;
+    blocks += per_channel ? (int)f.c : 1;
+  }
+  return 0;
+}
+
+int vae2_bn_multi_reduce(int n, const vae2_bn_fin* fins, int mode, void* stream) {
+  const char* fn = "vae2_bn_multi_reduce";
+  VAE2_REQUIRE(n >= 0 && (n == 0 || fins) && mode >= 0 && mode <= 2, fn, "bad arguments");
+  for (int i = 0; i < n; ++i) {
+    const vae2_bn_fin& f = fins[i];
+    VAE2_REQUIRE(f.partials && f.rows > 0, fn, "missing partials");
+    VAE2_REQUIRE(mode != 0 || (f.save && (f.countp || f.count > 0)), fn, "missing save / count");
+    VAE2_REQUIRE((f.running_mean == nullptr) == (f.running_var == nullptr), fn,
+                 "running_mean and running_var must both be set or both be null");
+  }
+  for (int i0 = 0; i0 < n; i0 += kBnMaxLayers) {
+    FinMulti m;
+    int blocks;
+    int rc = bn_fin_pack(n, fins, i0, m, blocks, true, fn);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    if (mode == 0)
+      VAE2_LAUNCH(reduce_then_multi_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else if (mode == 1)
+      VAE2_LAUNCH(reduce_then_multi_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else
+      VAE2_LAUNCH(reduce_then_multi_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    rc = check_launch(fn);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int vae2_bn_multi_finalize(int n, const vae2_bn_fin* fins, void* stream) {
+  const char* fn = "vae2_bn_multi_finalize";
+  VAE2_REQUIRE(n >= 0 && (n == 0 || fins), fn, "bad arguments");
+  for (int i = 0; i < n; ++i)
+    VAE2_REQUIRE(fins[i].save && (fins[i].countp || fins[i].count > 0), fn,
+                 "missing save / count");
+  for (int i0 = 0; i0 < n; i0 += kBnMaxLayers) {
+    FinMulti m;
+    int blocks;
+    int rc = bn_fin_pack(n, fins, i0, m, blocks, false, fn);
+    if (rc) return rc;
+    VAE2_LAUNCH(bn_finalize_multi_kernel, dim3((unsigned)m.n), dim3(256), 0, as_stream(stream), m);
+    rc = check_launch(fn);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -15,6 +15,15 @@ void set_error(const std::string& msg);
 int fail(const char* fn, const std::string& msg);  // returns -22
 int check_launch(const char* fn);                   // hipGetLastError -> code
 
+// Kernel launch log (vae2_kernel_log): every launch site goes through VAE2_LAUNCH so a
+// profiler can attribute the time of each C-ABI call to the kernels it launched.
+void note_kernel(const void* host_fn);
+#define VAE2_LAUNCH(K, ...)                                         \
+  do {                                                              \
+    ::vae2::note_kernel(reinterpret_cast<const void*>(K));          \
+    hipLaunchKernelGGL(K, __VA_ARGS__);                             \
+  } while (0)
+
 #define VAE2_REQUIRE(cond, fn, msg)          \
   do {                                       \
     if (!(cond)) return ::vae2::fail(fn, msg); \

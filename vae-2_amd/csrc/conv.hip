@@ -584,7 +584,7 @@ template <int TM, bool VEC, int ROLE, int KS = 1>
 static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((igemm_kernel<TM, T, VEC, ROLE, KS>), grid, dim3(256), 0, s, p); break;
+  case T: VAE2_LAUNCH((igemm_kernel<TM, T, VEC, ROLE, KS>), grid, dim3(256), 0, s, p); break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
@@ -594,7 +594,7 @@ template <bool VEC, int ROLE>
 static void launch_wide(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((igemm_kernel<2, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
+  case T: VAE2_LAUNCH((igemm_kernel<2, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
     CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
 #undef CASE
   }
@@ -1070,10 +1070,10 @@ template <int TM>
 static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)3 * TM * 4 * 4 * 64 * sizeof(float) / 4 * tn;  // 3 waves x NV x 64
   switch (tn) {
-    case 1: hipLaunchKernelGGL((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p); break;
-    case 2: hipLaunchKernelGGL((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p); break;
-    case 3: hipLaunchKernelGGL((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p); break;
-    default: hipLaunchKernelGGL((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p); break;
+    case 1: VAE2_LAUNCH((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p); break;
+    case 2: VAE2_LAUNCH((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p); break;
+    case 3: VAE2_LAUNCH((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p); break;
+    default: VAE2_LAUNCH((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p); break;
   }
 }
 
@@ -1148,7 +1148,7 @@ template <int TM, bool FLIP>
 static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p); break;
+  case T: VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p); break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
@@ -1244,12 +1244,12 @@ template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
                              hipStream_t s) {
   if (ks == 1) {  // 1x1: at most 64 channels = 4 column tiles per slab, one per wave
-    hipLaunchKernelGGL((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
+    VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
     return;
   }
   switch (tn) {
 #define CASE(T) \
-  case T: hipLaunchKernelGGL((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p); break;
+  case T: VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
 #undef CASE
   }
@@ -1288,7 +1288,7 @@ int vae2_conv2d_pack_weight_ld(const float* w, int64_t cout, int64_t cin, int k,
                "bad arguments");
   VAE2_REQUIRE(ld >= cin * k * k && ld < (int64_t(1) << 31), fn, "bad row stride");
   int64_t total = vae2_conv2d_packed_size(cout, cin, k, mode);
-  hipLaunchKernelGGL(pack_weight_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0,
+  VAE2_LAUNCH(pack_weight_kernel, dim3(ew_blocks(total, 256, 2048)), dim3(256), 0,
                      as_stream(stream), w, (int)cout, (int)cin, k * k, mode, (int)ld, out);
   return check_launch(fn);
 }
@@ -1301,7 +1301,7 @@ int vae2_conv2d_pack_weight(const float* w, int64_t cout, int64_t cin, int k, in
 int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* stream) {
   const char* fn = "vae2_conv2d_pack_weights";
   VAE2_REQUIRE(jobs && njobs > 0 && njobs <= 65535, fn, "bad job table");
-  hipLaunchKernelGGL(pack_weights_batched_kernel, dim3(32, (unsigned)njobs), dim3(256), 0,
+  VAE2_LAUNCH(pack_weights_batched_kernel, dim3(32, (unsigned)njobs), dim3(256), 0,
                      as_stream(stream), jobs);
   return check_launch(fn);
 }
@@ -1509,7 +1509,7 @@ int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* d
   }
 reduce:
   int64_t slab = dyd->c * (int64_t)ncol4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,
+  VAE2_LAUNCH(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,
                      (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw, dw_ld,
                      accumulate);
   int rc = check_launch(fn);

@@ -273,11 +273,11 @@ int vae2_l1_fwd(const float* p, const vae2_act* pd, const float* t,
   int64_t total = act_elems(pd);
   unsigned nb = reduce_blocks(total);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(l1_partials_kernel, dim3(nb), dim3(256), 0, s, p, to_act(pd), t,
+  VAE2_LAUNCH(l1_partials_kernel, dim3(nb), dim3(256), 0, s, p, to_act(pd), t,
                      to_act(td), ws, FastDiv((uint32_t)pd->c));
   int rc = check_launch(fn);
   if (rc) return rc;
-  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
+  VAE2_LAUNCH(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
                      scale, out, 0);
   return check_launch(fn);
 }
@@ -289,7 +289,7 @@ int vae2_l1_bwd(const float* p, const vae2_act* pd, const float* t,
   VAE2_REQUIRE(p && t && gout && dp && act_ok(pd) && act_ok(td) && act_ok(dpd), fn,
                "bad arguments");
   int64_t total = act_elems(pd);
-  hipLaunchKernelGGL(l1_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), p,
+  VAE2_LAUNCH(l1_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), p,
                      to_act(pd), t, to_act(td), gout, scale, dp, to_act(dpd), beta,
                      FastDiv((uint32_t)pd->c));
   return check_launch(fn);
@@ -302,11 +302,11 @@ int vae2_lsgan_fwd(const float* x, const vae2_act* xd, float target, float scale
   const int64_t total = act_elems(xd);
   const unsigned nb = reduce_blocks(total);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(sqdiff_partials_kernel, dim3(nb), dim3(256), 0, s, x, to_act(xd), target,
+  VAE2_LAUNCH(sqdiff_partials_kernel, dim3(nb), dim3(256), 0, s, x, to_act(xd), target,
                      ws, FastDiv((uint32_t)xd->c));
   int rc = check_launch(fn);
   if (rc) return rc;
-  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
+  VAE2_LAUNCH(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
                      scale, out, 0);
   return check_launch(fn);
 }
@@ -318,7 +318,7 @@ int vae2_lsgan_bwd(const float* x, const vae2_act* xd, float target, const float
   VAE2_REQUIRE(dxd->n == xd->n && dxd->h == xd->h && dxd->w == xd->w && dxd->c == xd->c, fn,
                "dx shape mismatch");
   const int64_t total = act_elems(xd);
-  hipLaunchKernelGGL(sqdiff_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+  VAE2_LAUNCH(sqdiff_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
                      x, to_act(xd), target, gout, scale, dx, to_act(dxd), beta,
                      FastDiv((uint32_t)xd->c));
   return check_launch(fn);
@@ -335,11 +335,11 @@ int vae2_reparam_kl_fwd(const float* muvar, const vae2_act* md,
   int64_t total = act_elems(zd);
   unsigned nb = reduce_blocks(total);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(reparam_kl_kernel, dim3(nb), dim3(256), 0, s, muvar, to_act(md), eps,
+  VAE2_LAUNCH(reparam_kl_kernel, dim3(nb), dim3(256), 0, s, muvar, to_act(md), eps,
                      to_act(ed), z, to_act(zd), prior, ws, FastDiv((uint32_t)zd->c));
   int rc = check_launch(fn);
   if (rc) return rc;
-  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
+  VAE2_LAUNCH(finish_sum_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, (int)nb,
                      scale, kl_out, accumulate);
   return check_launch(fn);
 }
@@ -354,7 +354,7 @@ int vae2_reparam_kl_bwd(const float* muvar, const vae2_act* md,
   VAE2_REQUIRE(!dz || act_ok(dzd), fn, "bad dz descriptor");
   int64_t total = act_elems(ed);
   Act dza = dz ? to_act(dzd) : to_act(ed);
-  hipLaunchKernelGGL(reparam_kl_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(reparam_kl_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), muvar, to_act(md), eps, to_act(ed), dz, dza, gkl, scale,
                      dmuvar, to_act(dmd), FastDiv((uint32_t)ed->c));
   return check_launch(fn);
@@ -371,7 +371,7 @@ int vae2_weighted_sum(int n, const float* const* terms, const float* lambdas,
     w.t[i] = terms[i];
     w.l[i] = lambdas[i];
   }
-  hipLaunchKernelGGL(weighted_sum_kernel, dim3(1), dim3(64), 0, as_stream(stream), w, total);
+  VAE2_LAUNCH(weighted_sum_kernel, dim3(1), dim3(64), 0, as_stream(stream), w, total);
   return check_launch(fn);
 }
 
@@ -380,7 +380,7 @@ int vae2_nonfinite_check(const float* x, int64_t n, int32_t* flag,
   const char* fn = "vae2_nonfinite_check";
   VAE2_REQUIRE(x && flag && n >= 0, fn, "bad arguments");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(nonfinite_kernel, dim3(ew_blocks(n, 256, 1024)), dim3(256), 0,
+  VAE2_LAUNCH(nonfinite_kernel, dim3(ew_blocks(n, 256, 1024)), dim3(256), 0,
                      as_stream(stream), x, n, flag);
   return check_launch(fn);
 }
@@ -395,7 +395,7 @@ int vae2_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
   double bc2 = 1.0 - pow((double)beta2, (double)step);
   float lr_corr = (float)((double)lr / bc1);
   float bc2s = (float)sqrt(bc2);
-  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
+  VAE2_LAUNCH(adam_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
                      as_stream(stream), p, g, m, v, n, lr_corr, beta1, beta2, eps,
                      weight_decay, bc2s);
   return check_launch(fn);
@@ -405,7 +405,7 @@ int vae2_adam_coeffs(double* state, float beta1, float beta2, float* coeffs,
                      void* stream) {
   const char* fn = "vae2_adam_coeffs";
   VAE2_REQUIRE(state && coeffs, fn, "null pointer");
-  hipLaunchKernelGGL(adam_coeffs_kernel, dim3(1), dim3(1), 0, as_stream(stream), state, beta1,
+  VAE2_LAUNCH(adam_coeffs_kernel, dim3(1), dim3(1), 0, as_stream(stream), state, beta1,
                      beta2, coeffs);
   return check_launch(fn);
 }
@@ -416,7 +416,7 @@ int vae2_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n,
   const char* fn = "vae2_adam_step_dev";
   VAE2_REQUIRE(p && g && m && v && coeffs && n >= 0, fn, "bad arguments");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
+  VAE2_LAUNCH(adam_dev_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
                      as_stream(stream), p, g, m, v, n, coeffs, beta1, beta2, eps, weight_decay);
   return check_launch(fn);
 }
@@ -426,7 +426,7 @@ int vae2_scale(float* dst, const float* src, int64_t n, float scale,
   const char* fn = "vae2_scale";
   VAE2_REQUIRE(dst && src && n >= 0, fn, "bad arguments");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(scale_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
+  VAE2_LAUNCH(scale_kernel, dim3(ew_blocks(n, 256, 4096)), dim3(256), 0,
                      as_stream(stream), dst, src, n, scale);
   return check_launch(fn);
 }

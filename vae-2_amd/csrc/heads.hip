@@ -614,10 +614,10 @@ static bool head_args_ok(const float* y, const vae2_act* yd, int cout2) {
 
 #define HEAD_DISPATCH(CO_, KERNEL, ...)                                   \
   switch (CO_) {                                                          \
-    case 1: hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); break;          \
-    case 2: hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__); break;          \
-    case 3: hipLaunchKernelGGL((KERNEL<3>), __VA_ARGS__); break;          \
-    default: hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__); break;         \
+    case 1: VAE2_LAUNCH((KERNEL<1>), __VA_ARGS__); break;          \
+    case 2: VAE2_LAUNCH((KERNEL<2>), __VA_ARGS__); break;          \
+    case 3: VAE2_LAUNCH((KERNEL<3>), __VA_ARGS__); break;          \
+    default: VAE2_LAUNCH((KERNEL<4>), __VA_ARGS__); break;         \
   }
 
 }  // namespace vae2
@@ -671,7 +671,7 @@ int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* sa
                 as_stream(stream), y, to_act(yd), save, w2, dout, to_act(doutd), ppb, rows, ws);
   int rc = check_launch(fn);
   if (rc) return rc;
-  hipLaunchKernelGGL(head_bwd_colsum_kernel, dim3((unsigned)ceil_div(NC, 64)), dim3(256), 0,
+  VAE2_LAUNCH(head_bwd_colsum_kernel, dim3((unsigned)ceil_div(NC, 64)), dim3(256), 0,
                      as_stream(stream), (const float*)ws, (int)blocks, C, cout2, sums, dgamma,
                      dbeta, dw2, db2);
   return check_launch(fn);
@@ -743,10 +743,10 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   dim3 grid((unsigned)(yd->n * yd->h * p.nxb * ceil_div(yd->c, kUsCB)));
   hipStream_t st = as_stream(stream);
   switch (nup) {
-    case 0: hipLaunchKernelGGL(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
-    case 1: hipLaunchKernelGGL(upsum_kernel<1>, grid, dim3(256), shm, st, p); break;
-    case 2: hipLaunchKernelGGL(upsum_kernel<2>, grid, dim3(256), shm, st, p); break;
-    default: hipLaunchKernelGGL(upsum_kernel<3>, grid, dim3(256), shm, st, p); break;
+    case 0: VAE2_LAUNCH(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
+    case 1: VAE2_LAUNCH(upsum_kernel<1>, grid, dim3(256), shm, st, p); break;
+    case 2: VAE2_LAUNCH(upsum_kernel<2>, grid, dim3(256), shm, st, p); break;
+    default: VAE2_LAUNCH(upsum_kernel<3>, grid, dim3(256), shm, st, p); break;
   }
   return check_launch(fn);
 }
@@ -794,14 +794,14 @@ int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n
   dim3 grid((unsigned)(dyd->n * dyd->h * p.nxb * cb));
   hipStream_t st = as_stream(stream);
   switch (n) {
-    case 1: hipLaunchKernelGGL(up_adj_h_kernel<1>, grid, dim3(256), shm, st, p); break;
-    case 2: hipLaunchKernelGGL(up_adj_h_kernel<2>, grid, dim3(256), shm, st, p); break;
-    default: hipLaunchKernelGGL(up_adj_h_kernel<3>, grid, dim3(256), shm, st, p); break;
+    case 1: VAE2_LAUNCH(up_adj_h_kernel<1>, grid, dim3(256), shm, st, p); break;
+    case 2: VAE2_LAUNCH(up_adj_h_kernel<2>, grid, dim3(256), shm, st, p); break;
+    default: VAE2_LAUNCH(up_adj_h_kernel<3>, grid, dim3(256), shm, st, p); break;
   }
   int rc = check_launch(fn);
   if (rc) return rc;
   for (int s = 0; s < n; ++s) {
-    hipLaunchKernelGGL(up_adj_v_kernel, dim3((unsigned)(dyd->n * p.zh[s]), cb), dim3(256), 0, st,
+    VAE2_LAUNCH(up_adj_v_kernel, dim3((unsigned)(dyd->n * p.zh[s]), cb), dim3(256), 0, st,
                        p, s);
     rc = check_launch(fn);
     if (rc) return rc;

@@ -9,8 +9,42 @@
 //   nn.AdaptiveAvgPool2d((1,1)) :1025                  -> global avgpool fwd / bwd
 #include "common.h"
 
+#include <cxxabi.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
 
 namespace vae2 {
+
+// ------------------------------------------------------ launch log ----
+static std::atomic<bool> g_klog{false};
+static thread_local std::vector<const void*> g_klog_v;
+
+void note_kernel(const void* host_fn) {
+  if (g_klog.load(std::memory_order_relaxed)) g_klog_v.push_back(host_fn);
+}
+
+// "void vae2::dconv3_kernel<4, 2, false>(vae2::DConv)" -> "dconv3_kernel<4, 2, false>"
+static std::string kernel_label(const void* fn) {
+  const char* raw = hipKernelNameRefByPtr(fn, nullptr);
+  if (!raw) return "?";
+  int st = 0;
+  char* dem = abi::__cxa_demangle(raw, nullptr, nullptr, &st);
+  std::string s = (st == 0 && dem) ? dem : raw;
+  std::free(dem);
+  if (s.rfind("void ", 0) == 0) s = s.substr(5);
+  int depth = 0;
+  for (size_t i = 0; i < s.size(); ++i) {  // drop the parameter list
+    if (s[i] == '<') ++depth;
+    if (s[i] == '>') --depth;
+    if (s[i] == '(' && depth == 0) { s = s.substr(0, i); break; }
+  }
+  size_t pos;
+  while ((pos = s.find("vae2::")) != std::string::npos) s.erase(pos, 6);
+  return s;
+}
 
 // ------------------------------------------------------------- errors ----
 static thread_local std::string g_last_error;
@@ -338,12 +372,12 @@ static int spatial_sum(const float* x, const vae2_act* xd, float* out, int64_t o
   int64_t ppb = 0;
   int64_t chunks = spatial_chunks(xd, &ppb);
   VAE2_REQUIRE(part && ws_size >= xd->n * chunks * xd->c, fn, "workspace too small");
-  hipLaunchKernelGGL(spatial_partials_kernel, dim3((unsigned)chunks, (unsigned)xd->n),
+  VAE2_LAUNCH(spatial_partials_kernel, dim3((unsigned)chunks, (unsigned)xd->n),
                      dim3(256), 0, s, x, to_act(xd), ppb, part);
   int rc = check_launch(fn);
   if (rc) return rc;
   int64_t nc = xd->n * xd->c;
-  hipLaunchKernelGGL(spatial_finish_kernel, dim3((unsigned)ceil_div(nc, 256)), dim3(256), 0, s,
+  VAE2_LAUNCH(spatial_finish_kernel, dim3((unsigned)ceil_div(nc, 256)), dim3(256), 0, s,
                      (const float*)part, chunks, xd->n, xd->c, out, os, scale, accumulate);
   return check_launch(fn);
 }
@@ -399,6 +433,28 @@ int vae2_abi_version(void) { return VAE2_ABI_VERSION; }
 
 const char* vae2_last_error(void) { return g_last_error.c_str(); }
 
+int vae2_kernel_log(int enable) {
+  g_klog.store(enable != 0);
+  g_klog_v.clear();
+  return 0;
+}
+
+int64_t vae2_kernel_log_read(char* buf, int64_t len) {
+  std::string out;
+  for (size_t i = 0; i < g_klog_v.size(); ++i) {
+    if (i) out += ';';
+    out += kernel_label(g_klog_v[i]);
+  }
+  const int64_t n = (int64_t)g_klog_v.size();
+  g_klog_v.clear();
+  if (buf && len > 0) {
+    const size_t m = out.size() < (size_t)(len - 1) ? out.size() : (size_t)(len - 1);
+    std::memcpy(buf, out.data(), m);
+    buf[m] = 0;
+  }
+  return n;
+}
+
 int vae2_upsample_bilinear_fwd(const float* x, const vae2_act* xd, float* y,
                                const vae2_act* yd, float beta, void* stream) {
   const char* fn = "vae2_upsample_bilinear_fwd";
@@ -406,7 +462,7 @@ int vae2_upsample_bilinear_fwd(const float* x, const vae2_act* xd, float* y,
   VAE2_REQUIRE(xd->n == yd->n && xd->c == yd->c, fn, "n / c mismatch");
   int64_t total = act_elems(yd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
-  hipLaunchKernelGGL(upsample_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(upsample_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), x, to_act(xd), y, to_act(yd), beta,
                      FastDiv((uint32_t)yd->c), FastDiv((uint32_t)yd->w),
                      FastDiv((uint32_t)yd->h));
@@ -423,13 +479,13 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
                "tensor too large");
   if (dyd->ps % 4 == 0 && (uintptr_t)dy % 16 == 0) {
     const int64_t quads = act_elems(dxd) / dxd->c * ((dxd->c + 3) / 4);
-    hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(ew_blocks(quads)), dim3(256), 0,
+    VAE2_LAUNCH(upsample_bwd4_kernel, dim3(ew_blocks(quads)), dim3(256), 0,
                        as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
                        FastDiv((uint32_t)((dxd->c + 3) / 4)), FastDiv((uint32_t)dxd->w),
                        FastDiv((uint32_t)dxd->h));
     return check_launch(fn);
   }
-  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(upsample_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
                      FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)dxd->w),
                      FastDiv((uint32_t)dxd->h));
@@ -451,7 +507,7 @@ int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
   }
   int64_t total = act_elems(yd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
-  hipLaunchKernelGGL(fuse_sum_relu_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(fuse_sum_relu_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), t, y, to_act(yd), FastDiv((uint32_t)yd->c),
                      FastDiv((uint32_t)yd->w), FastDiv((uint32_t)yd->h));
   return check_launch(fn);
@@ -465,7 +521,7 @@ int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,
   VAE2_REQUIRE(same_hw(dyd, yd) && same_hw(yd, gd) && dyd->c == yd->c && gd->c == yd->c, fn,
                "shape mismatch");
   int64_t total = act_elems(yd);
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+  VAE2_LAUNCH(relu_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
                      dy, to_act(dyd), y, to_act(yd), g, to_act(gd), FastDiv((uint32_t)yd->c));
   return check_launch(fn);
 }
@@ -476,7 +532,7 @@ int vae2_copy_act(const float* x, const vae2_act* xd, float* y,
   VAE2_REQUIRE(x && y && act_ok(xd) && act_ok(yd), fn, "bad arguments");
   VAE2_REQUIRE(same_hw(xd, yd) && xd->c == yd->c, fn, "shape mismatch");
   int64_t total = act_elems(xd);
-  hipLaunchKernelGGL(copy_act_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+  VAE2_LAUNCH(copy_act_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
                      x, to_act(xd), y, to_act(yd), beta, FastDiv((uint32_t)xd->c));
   return check_launch(fn);
 }
@@ -486,7 +542,7 @@ int vae2_codemap_tile_fwd(const float* v, int64_t vs, float* y,
   const char* fn = "vae2_codemap_tile_fwd";
   VAE2_REQUIRE(v && y && act_ok(yd) && vs >= yd->c, fn, "bad arguments");
   int64_t total = act_elems(yd);
-  hipLaunchKernelGGL(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), v,
+  VAE2_LAUNCH(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), v,
                      vs, y, to_act(yd), 1.f, 0.f, FastDiv((uint32_t)yd->c),
                      FastDiv((uint32_t)(yd->h * yd->w)));
   return check_launch(fn);
@@ -510,7 +566,7 @@ int vae2_nchw_to_nhwc(const float* x, float* y, const vae2_act* yd,
   const char* fn = "vae2_nchw_to_nhwc";
   VAE2_REQUIRE(x && y && act_ok(yd), fn, "bad arguments");
   int64_t total = act_elems(yd);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), x, y, to_act(yd), beta, FastDiv((uint32_t)yd->c),
                      FastDiv((uint32_t)(yd->h * yd->w)));
   return check_launch(fn);
@@ -521,7 +577,7 @@ int vae2_nhwc_to_nchw(const float* x, const vae2_act* xd, float* y,
   const char* fn = "vae2_nhwc_to_nchw";
   VAE2_REQUIRE(x && y && act_ok(xd), fn, "bad arguments");
   int64_t total = act_elems(xd);
-  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  VAE2_LAUNCH(nhwc_to_nchw_kernel, dim3(ew_blocks(total)), dim3(256), 0,
                      as_stream(stream), x, to_act(xd), y, beta, FastDiv((uint32_t)xd->c),
                      FastDiv((uint32_t)(xd->h * xd->w)));
   return check_launch(fn);
@@ -545,7 +601,7 @@ int vae2_global_avgpool_bwd(const float* dy, const vae2_act* dyd, float* dx,
   VAE2_REQUIRE(dyd->h == 1 && dyd->w == 1 && dyd->n == dxd->n && dyd->c == dxd->c, fn,
                "dy must be (n, 1, 1, c)");
   int64_t total = act_elems(dxd);
-  hipLaunchKernelGGL(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), dy,
+  VAE2_LAUNCH(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), dy,
                      dyd->ps, dx, to_act(dxd), 1.f / (float)(dxd->h * dxd->w), beta,
                      FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)(dxd->h * dxd->w)));
   return check_launch(fn);

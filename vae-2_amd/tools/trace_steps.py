@@ -12,21 +12,13 @@ top --instances kernel instantiations by time.
 import argparse
 import csv
 import json
+import os
 import re
+import sys
 from collections import defaultdict
 
-FAMILIES = (  # (family, regex on the demangled kernel name), first match wins
-    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false>|igemm_kernel<\d+, \d+, \w+, 0"),
-    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true>|igemm_kernel<\d+, \d+, \w+, [12]"),
-    ("conv_wgrad", r"wgrad"),
-    ("batchnorm", r"bn_|reduce_then|chan_partials|bn_stats|bnfin"),
-    ("heads", r"upsum|head_|up_adj"),
-    ("fuse_resample", r"upsample|fuse_sum|relu_bwd|copy_act|tile_kernel|spatial_|codemap"),
-    ("optimizer", r"adam|pack_weight"),
-    ("loss_elbo", r"l1_|reparam|weighted_sum|finish_sum|scale_kernel|nonfinite|nchw|nhwc"),
-    ("torch_aten", r"at::native|^at::"),
-    ("copies", r"rocclr_copy|rocclr_fill"),
-)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from vae2.prof import family  # noqa: E402  (the families bench.py reports live)
 
 
 def kernel_name(name):
@@ -41,13 +33,6 @@ def short(n):
         m = re.search(r"CUDAFunctor_(\w+)|(\w+Functor)|(direct_copy)", n)
         return "torch:" + (next(g for g in m.groups() if g) if m else n[:40])
     return re.sub(r"<.*", "", n)
-
-
-def family(n):
-    for f, rx in FAMILIES:
-        if re.search(rx, n):
-            return f
-    return "other"
 
 
 def load(path):

@@ -27,10 +27,29 @@ class Act(ctypes.Structure):
 
 P_ACT = ctypes.POINTER(Act)
 
+
+class BnLayer(ctypes.Structure):
+    """vae2_bn_layer (include/vae2_hip.h): one layer of a multi-layer BN launch."""
+    _fields_ = [("x", c_vp), ("xd", Act), ("a", c_vp), ("ad", Act), ("o", c_vp), ("od", Act),
+                ("dy", c_vp), ("dyd", Act), ("dres", c_vp), ("dresd", Act),
+                ("save", c_vp), ("gamma", c_vp), ("partials", c_vp), ("sums", c_vp),
+                ("countp", c_vp), ("count", c_f64), ("relu", c_int)]
+
+
+class BnFin(ctypes.Structure):
+    """vae2_bn_fin (include/vae2_hip.h): one layer of a multi-layer BN reduction."""
+    _fields_ = [("partials", c_vp), ("rows", c_i64), ("c", c_i64), ("sums", c_vp),
+                ("countp", c_vp), ("count", c_f64), ("gamma", c_vp), ("beta", c_vp),
+                ("running_mean", c_vp), ("running_var", c_vp), ("num_batches_tracked", c_vp),
+                ("momentum", c_f32), ("eps", c_f32), ("save", c_vp), ("dgamma", c_vp),
+                ("dbeta", c_vp)]
+
 # name -> (restype, argtypes)
 _SIGS = {
     "vae2_abi_version": (c_int, []),
     "vae2_last_error": (ctypes.c_char_p, []),
+    "vae2_kernel_log": (c_int, [c_int]),
+    "vae2_kernel_log_read": (c_i64, [ctypes.c_char_p, c_i64]),
     "vae2_conv2d_packed_size": (c_i64, [c_i64, c_i64, c_int, c_int]),
     "vae2_conv2d_pack_weight": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp]),
     "vae2_conv2d_pack_weight_ld": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_i64, c_vp, c_vp]),
@@ -90,6 +109,11 @@ _SIGS = {
     "vae2_reduce_ws_size": (c_i64, [c_i64]),
     "vae2_l1_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp, c_vp, c_vp]),
     "vae2_l1_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_f32, c_vp, P_ACT, c_f32, c_vp]),
+    "vae2_bn_multi_apply": (c_int, [c_int, c_vp, c_vp]),
+    "vae2_bn_multi_bwd_reduce": (c_int, [c_int, c_vp, c_vp]),
+    "vae2_bn_multi_bwd_apply": (c_int, [c_int, c_vp, c_vp]),
+    "vae2_bn_multi_reduce": (c_int, [c_int, c_vp, c_int, c_vp]),
+    "vae2_bn_multi_finalize": (c_int, [c_int, c_vp, c_vp]),
     "vae2_lsgan_fwd": (c_int, [c_vp, P_ACT, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "vae2_lsgan_bwd": (c_int, [c_vp, P_ACT, c_f32, c_vp, c_f32, c_vp, P_ACT, c_f32, c_vp]),
     "vae2_reparam_kl_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_int, c_f32, c_vp,
@@ -107,7 +131,7 @@ _SIGS = {
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 
 
@@ -153,5 +177,12 @@ def check(rc):
         raise HipError(f"libvae2_hip error {rc}: {msg.decode() if msg else ''}")
 
 
+CALL_HOOK = None  # vae2.prof.StepProfiler._call while a profiler is active
+
+
 def call(name, *args):
-    check(getattr(load(), name)(*args))
+    fn = getattr(load(), name)
+    if CALL_HOOK is not None:
+        check(CALL_HOOK(name, fn, args))
+    else:
+        check(fn(*args))

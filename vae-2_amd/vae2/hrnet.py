@@ -102,6 +102,27 @@ def _run_convbn_seq(seq, x, x_link=None):
     return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2, x_link=x_link)
 
 
+def _run_convbn_seqs(seqs, xs):
+    """Independent Sequential(Conv2d, BatchNorm2d[, ReLU]) units of one depth level,
+    their BatchNorm steps in shared launches (ops.conv_bn_multi)."""
+    if not seqs:
+        return []
+    return ops.conv_bn_multi(xs, [q[0] for q in seqs], [q[1] for q in seqs],
+                             [len(q) > 2 for q in seqs])
+
+
+def run_blocks_lockstep(blocks, xs):
+    """One residual block per branch (same depth in a HighResolutionModule), in lockstep:
+    conv1 of every branch, then conv2 + residual of every branch, BatchNorm batched."""
+    if not all(isinstance(b, BasicBlock) and b.downsample is None for b in blocks):
+        return [b.run(x) for b, x in zip(blocks, xs)]
+    links = [ops.GradLink(2) for _ in blocks]  # x feeds conv1 and the shortcut
+    outs = ops.conv_bn_multi(xs, [b.conv1 for b in blocks], [b.bn1 for b in blocks], True,
+                             x_links=links)
+    return ops.conv_bn_multi(outs, [b.conv2 for b in blocks], [b.bn2 for b in blocks], True,
+                             residuals=xs, res_links=links)
+
+
 def _shortcut(cin, cout, stride):
     if stride == 1 and cin == cout:
         return None
@@ -187,23 +208,35 @@ class HighResolutionModule(nn.Module):
         return self.num_inchannels
 
     def run(self, xs):
-        xs = [run_seq(self.branches[b], xs[b]) for b in range(self.num_branches)]
-        if self.num_branches == 1:
+        nb = self.num_branches
+        depths = {len(self.branches[b]) for b in range(nb)}
+        if len(depths) == 1:  # branches in lockstep (enc_hrnet.py:226-231)
+            for d in range(depths.pop()):
+                xs = run_blocks_lockstep([self.branches[b][d] for b in range(nb)], xs)
+        else:
+            xs = [run_seq(self.branches[b], xs[b]) for b in range(nb)]
+        if nb == 1:
             return xs
+        # fuse (enc_hrnet.py:233-249): every j > i 1x1 conv + BN in one batch (upsampled
+        # in the fuse kernel), the j < i stride-2 chains batched by chain position
+        rows = list(enumerate(self.fuse_layers))
+        terms = {}
+        ups = [(i, j) for i, _ in rows for j in range(nb) if j > i]
+        for (i, j), t in zip(ups, _run_convbn_seqs([self.fuse_layers[i][j] for i, j in ups],
+                                                  [xs[j] for _, j in ups])):
+            terms[(i, j)] = t
+        downs = [(i, j) for i, _ in rows for j in range(nb) if j < i]
+        cur = {(i, j): xs[j] for i, j in downs}
+        for k in range(max((i - j for i, j in downs), default=0)):
+            live = [(i, j) for i, j in downs if k < i - j]
+            outs = _run_convbn_seqs([self.fuse_layers[i][j][k] for i, j in live],
+                                    [cur[ij] for ij in live])
+            cur.update(zip(live, outs))
+        terms.update(cur)
         out = []
-        for i, row in enumerate(self.fuse_layers):
-            terms = []
-            for j in range(self.num_branches):
-                if j == i:
-                    terms.append(xs[j])
-                elif j > i:  # 1x1 conv + BN at branch j's resolution; upsampled in the fuse kernel
-                    terms.append(_run_convbn_seq(row[j], xs[j]))
-                else:
-                    t = xs[j]
-                    for unit in row[j]:
-                        t = _run_convbn_seq(unit, t)
-                    terms.append(t)
-            out.append(ops.fuse_sum_relu(terms, xs[i].shape[1:3]))
+        for i, _ in rows:
+            out.append(ops.fuse_sum_relu([xs[j] if j == i else terms[(i, j)] for j in range(nb)],
+                                         xs[i].shape[1:3]))
         return out
 
 
@@ -243,19 +276,17 @@ def make_stage(cfg, num_inchannels, multi_scale_output=True):
 
 
 def run_transition(trans, ys, nbranches):
-    """Branch inputs of the next stage from the previous stage's outputs."""
-    xs = []
-    for i in range(nbranches):
-        t = trans[i]
-        if t is None:
-            xs.append(ys[i])
-        elif i < len(ys):
-            xs.append(_run_convbn_seq(t, ys[i]))
-        else:
-            x = ys[-1]
-            for unit in t:
+    """Branch inputs of the next stage from the previous stage's outputs; the first
+    conv+BN unit of every transition in one batch."""
+    xs = [ys[i] if trans[i] is None else None for i in range(nbranches)]
+    todo = [i for i in range(nbranches) if trans[i] is not None]
+    firsts = [trans[i] if i < len(ys) else trans[i][0] for i in todo]
+    outs = _run_convbn_seqs(firsts, [ys[i] if i < len(ys) else ys[-1] for i in todo])
+    for i, x in zip(todo, outs):
+        if i >= len(ys):
+            for unit in list(trans[i])[1:]:
                 x = _run_convbn_seq(unit, x)
-            xs.append(x)
+        xs[i] = x
     return xs
 
 
@@ -353,7 +384,7 @@ class HighResolutionNet(nn.Module):
     def _apply_codes(self, prefix, xs, codes):
         """cat((code maps..., x_b)) -> transition3_e (enc_hrnet.py:818-830, :880-888)."""
         trans = getattr(self, prefix + "transition3_e")
-        out = []
+        xes = []
         for b, x in enumerate(xs):
             parts, tiles = [], []
             for c in codes:
@@ -365,10 +396,10 @@ class HighResolutionNet(nn.Module):
                     tiles.append(True)
             parts.append(x)
             tiles.append(False)
-            xe = ops.cat(parts, x.shape[1:3], tiles)
-            t = trans[b]
-            out.append(xe if t is None else _run_convbn_seq(t, xe))
-        return out
+            xes.append(ops.cat(parts, x.shape[1:3], tiles))
+        todo = [b for b in range(len(xs)) if trans[b] is not None]
+        outs = dict(zip(todo, _run_convbn_seqs([trans[b] for b in todo], [xes[b] for b in todo])))
+        return [outs.get(b, xes[b]) for b in range(len(xs))]
 
     def _heads(self, prefix, ys):
         heads = [getattr(self, f"{prefix}last_layer_{k}") for k in (1, 2, 3)]

@@ -271,6 +271,14 @@ def packed_weight_cols(weight, split, j, mode):
     return out
 
 
+def _conv_work(kind, xa, yshape, k, stride):
+    """prof.note for a conv call: 2*M*N*K FLOPs; input, output and weights moved once."""
+    n, oh, ow, cout = yshape
+    prof.note(2.0 * n * oh * ow * cout * xa.c * k * k,
+              4.0 * (xa.n * xa.h * xa.w * xa.c + n * oh * ow * cout + cout * xa.c * k * k),
+              prof.conv_label(kind, xa.c, cout, k, stride, xa.h, xa.w))
+
+
 def _conv_fwd(x, weight, bias, spec, stats=None):
     xp, xa = act_of(x)
     n, h, w, _ = x.shape
@@ -278,18 +286,11 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     cout = weight.shape[0]
     y = new_act((n, oh, ow, cout), x)
     yp, ya = act_of(y)
-    timer = prof.active()
-    ev = None
-    if timer is not None and timer.matches(xa, (n, oh, ow, cout), spec):
-        # algorithmic: 2*M*N*K flops; bytes = input read once + output written once + weights
-        ev = timer.record(2.0 * n * oh * ow * cout * xa.c * spec.k * spec.k,
-                          4.0 * (n * h * w * xa.c + n * oh * ow * cout +
-                                 cout * xa.c * spec.k * spec.k))
     wp = packed_weight(weight, 0)
+    if prof.active():
+        _conv_work("fwd", xa, (n, oh, ow, cout), spec.k, spec.stride)
     call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(wp), ptr(bias), yp, ctypes.byref(ya),
          spec.k, spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
-    if ev is not None:
-        timer.finish(ev)
     return y
 
 
@@ -306,6 +307,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
         size = _lib.load().vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xa), ctypes.byref(dya),
                                                           spec.k)
         ws = _empty((max(size, 1),), x)
+        if prof.active():
+            _conv_work("wgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya), ptr(wsink),
              ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
     dx = None
@@ -320,6 +323,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
                 link.buf = dx
         dxp, dxa = act_of(dx)
         wp = packed_weight(weight, 1)
+        if prof.active():
+            _conv_work("dgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp, ctypes.byref(dxa),
              spec.k, spec.stride, spec.pad, beta, s)
         if link is not None:
@@ -377,6 +382,8 @@ class _ConvBN(torch.autograd.Function):
             resp, resa = act_of(residual)
         else:
             resp, resa = None, ya
+        if prof.active():  # read r (+ residual), write y
+            prof.note(0, 4.0 * r.numel() * (3 if residual is not None else 2))
         call("vae2_bn_apply", rp, ctypes.byref(ra), ptr(save), resp, ctypes.byref(resa), yp,
              ctypes.byref(ya), int(spec.relu), s)
         ctx.spec = spec
@@ -405,6 +412,8 @@ class _ConvBN(torch.autograd.Function):
             yp = None  # the kernels recompute the ReLU mask from r (no read of y)
         rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
         part = _empty((2 * rows * cout,), r)
+        if prof.active():  # read dy, r (+ y)
+            prof.note(0, 4.0 * r.numel() * (3 if yp is not None else 2))
         call("vae2_bn_relu_bwd_reduce", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
              ctypes.byref(ra), ptr(save), int(spec.relu), ptr(part), s)
         lsums = _empty((2 * cout,), r, torch.float64)
@@ -422,6 +431,9 @@ class _ConvBN(torch.autograd.Function):
             dresp, dresa = act_of(dres)
         else:
             dresp, dresa = None, dra
+        if prof.active():  # read dy, r (+ y); write dr (+ dres)
+            prof.note(0, 4.0 * r.numel() * (3 + (1 if yp is not None else 0) +
+                                             (1 if dres is not None else 0)))
         call("vae2_bn_relu_bwd_apply", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), rp,
              ctypes.byref(ra), ptr(save), ptr(gamma), ptr(gsums), ctx.count, int(spec.relu), drp,
              ctypes.byref(dra), dresp, ctypes.byref(dresa), s)
@@ -438,10 +450,230 @@ class _ConvBN(torch.autograd.Function):
 
 def conv_bn(x, conv, bn, relu, residual=None, x_link=None, res_link=None):
     """relu?(bn(conv(x)) + residual) with training-mode (or eval-mode) BatchNorm.
-    x_link / res_link: GradLink shared with the other consumer(s) of x / residual."""
+    x_link / res_link: GradLink shared with the other consumer(s) of x / residual.
+    Training mode goes through the multi-layer path (one layer); eval mode, and
+    residual views the multi-layer kernels cannot take, through _ConvBN."""
     spec = ConvSpec(conv, bn, relu)
     spec.x_link, spec.res_link = x_link, res_link
+    if spec.training and (residual is None or _bn_quad_ok(residual)):
+        return _ConvBNMulti.apply((spec,), x, conv.weight, conv.bias, bn.weight, bn.bias,
+                                  residual)[0]
     return _ConvBN.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec)
+
+
+def _bn_quad_ok(t):
+    """Eligible for the multi-layer BN kernels: 16-byte aligned, pixel stride % 4 == 0."""
+    p_, a = act_of(t)
+    return p_.value % 16 == 0 and a.ps % 4 == 0 and a.c <= 1024
+
+
+_COUNTS = {}
+
+
+def _counts_dev(counts, like):
+    """Device copy of per-layer element counts (cached: the SyncBN exchange appends
+    them to the statistics so the global count is the sum of the real local counts)."""
+    key = (tuple(counts), like.device)
+    t = _COUNTS.get(key)
+    if t is None:
+        t = torch.tensor(counts, dtype=torch.float64).to(like.device)
+        _COUNTS[key] = t
+    return t
+
+
+class _ConvBNMulti(torch.autograd.Function):
+    """n independent conv -> BatchNorm(train) [-> +residual] [-> ReLU] layers (one HRNet
+    depth level): the convs launch per layer, every BatchNorm step is one launch for all
+    n layers (vae2_bn_multi_*), and with SyncBN one exchange carries all n layers'
+    statistics and element counts.  flat = (x, weight, bias, gamma, beta, residual) per
+    layer."""
+
+    @staticmethod
+    def forward(ctx, specs, *flat):
+        lib = _lib.load()
+        s = stream_ptr()
+        n = len(specs)
+        L = [flat[6 * i:6 * i + 6] for i in range(n)]
+        group = _bn_group()
+        rs, saves, fins, counts, cs = [], [], [], [], []
+        for (x, weight, bias, gamma, beta, residual), spec in zip(L, specs):
+            nn_, h, w, _ = x.shape
+            oh, ow = spec.out_hw(h, w)
+            cout = weight.shape[0]
+            xp, xa = act_of(x)
+            rows = lib.vae2_conv2d_fwd_stats_rows(xp, ctypes.byref(xa),
+                                                  ctypes.byref(Act(nn_, oh, ow, cout, cout)),
+                                                  spec.k, spec.stride, spec.pad)
+            stats = _empty((2 * rows * cout,), x)
+            rs.append(_conv_fwd(x, weight, bias, spec, stats))
+            saves.append(_empty((4 * cout,), x))
+            counts.append(float(nn_ * oh * ow))
+            cs.append(cout)
+            fins.append((stats, rows))
+        tot = 2 * sum(cs)
+        buf = _empty((tot + n,), rs[0], torch.float64)
+        world = 1
+        if group is not None:
+            buf[tot:].copy_(_counts_dev(counts, buf))
+            world = dist.get_world_size(group)
+        arr = (_lib.BnFin * n)()
+        off = 0
+        for i, ((stats, rows), spec, c) in enumerate(zip(fins, specs, cs)):
+            bn = spec.bn
+            gamma, beta = L[i][3], L[i][4]
+            if counts[i] * world <= 1:
+                raise ValueError("Expected more than 1 value per channel when training, "
+                                 f"got input size {(counts[i], c)}")
+            track = bn.track_running_stats and bn.running_mean is not None
+            arr[i] = _lib.BnFin(
+                stats.data_ptr(), rows, c, buf.data_ptr() + 8 * off,
+                buf.data_ptr() + 8 * (tot + i) if group is not None else None, counts[i],
+                _p(gamma), _p(beta), _p(bn.running_mean) if track else None,
+                _p(bn.running_var) if track else None,
+                _p(bn.num_batches_tracked) if track else None, spec.momentum, spec.eps,
+                saves[i].data_ptr(), None, None)
+            off += 2 * c
+        if group is None:
+            call("vae2_bn_multi_reduce", n, arr, 0, s)
+        else:  # SyncBN: one exchange of every layer's (sum x, sum x^2) and count
+            call("vae2_bn_multi_reduce", n, arr, 2, s)
+            from . import dist as vdist
+            vdist.all_reduce_(buf, group=group)
+            call("vae2_bn_multi_finalize", n, arr, s)
+        ys = []
+        lay = (_lib.BnLayer * n)()
+        for i, (r, save, spec) in enumerate(zip(rs, saves, specs)):
+            y = new_act(tuple(r.shape), r)
+            ys.append(y)
+            res = L[i][5]
+            lay[i] = _bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
+                               spec.relu)
+        if prof.active():
+            prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None else 2)
+                             for i, r in enumerate(rs)))
+        call("vae2_bn_multi_apply", n, lay, s)
+        ctx.specs = specs
+        ctx.counts = counts
+        ctx.group = group
+        ctx.has_res = [l_[5] is not None for l_ in L]
+        ctx.params = [l_[1:5] for l_ in L]
+        ctx.save_for_backward(*[l_[0] for l_ in L], *rs, *ys, *saves)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        s = stream_ptr()
+        specs = ctx.specs
+        n = len(specs)
+        saved = ctx.saved_tensors
+        xs, rs, ys, saves = (saved[k * n:(k + 1) * n] for k in range(4))
+        need = ctx.needs_input_grad
+        cs = [int(r.shape[3]) for r in rs]
+        tot = 2 * sum(cs)
+        buf = _empty((tot + n,), rs[0], torch.float64)
+        group = ctx.group
+        if group is not None:
+            buf[tot:].copy_(_counts_dev(ctx.counts, buf))
+        lay = (_lib.BnLayer * n)()
+        fins = (_lib.BnFin * n)()
+        keep, drs, dress = [], [], []
+        off = 0
+        lib = _lib.load()
+        for i in range(n):
+            r, y, save, spec = rs[i], ys[i], saves[i], specs[i]
+            dy = dys[i]
+            dy = as_act(dy) if dy is not None else torch.zeros_like(y)
+            if not _bn_quad_ok(dy):  # e.g. a channel slice of a concatenation's gradient
+                dy = _aligned_copy(dy)
+            _, ra = act_of(r)
+            rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
+            part = _empty((2 * rows * cs[i],), r)
+            dr = new_act(tuple(r.shape), r)
+            dres = new_act(tuple(r.shape), r) if ctx.has_res[i] and need[1 + 6 * i + 5] else None
+            gamma, beta = ctx.params[i][2], ctx.params[i][3]
+            gsink, gret = _grad_sink(gamma, need[1 + 6 * i + 3])
+            bsink, bret = _grad_sink(beta, need[1 + 6 * i + 4])
+            sums_p = buf.data_ptr() + 8 * off
+            countp = buf.data_ptr() + 8 * (tot + i) if group is not None else None
+            lay[i] = _bn_layer(r, y if ctx.has_res[i] else None, dr, dy, dres, save, gamma,
+                               part, sums_p, countp, ctx.counts[i], spec.relu)
+            fins[i] = _lib.BnFin(part.data_ptr(), rows, cs[i], sums_p, None, ctx.counts[i],
+                                 None, None, None, None, None, 0.0, 0.0, None, _p(gsink),
+                                 _p(bsink))
+            keep.append((dy, part))
+            drs.append(dr)
+            dress.append((dres, gret, bret))
+            off += 2 * cs[i]
+        if prof.active():
+            prof.note(0, sum(4.0 * r.numel() * (3 if h_ else 2) for r, h_ in zip(rs, ctx.has_res)))
+        call("vae2_bn_multi_bwd_reduce", n, lay, s)
+        call("vae2_bn_multi_reduce", n, fins, 1, s)  # local sums + dgamma / dbeta
+        if group is not None:  # SyncBN: global (sum g, sum g*xhat) for the input gradients
+            from . import dist as vdist
+            vdist.all_reduce_(buf, group=group)
+        if prof.active():
+            prof.note(0, sum(4.0 * r.numel() * (3 + (1 if h_ else 0) + (1 if d[0] is not None else 0))
+                             for r, h_, d in zip(rs, ctx.has_res, dress)))
+        call("vae2_bn_multi_bwd_apply", n, lay, s)
+        grads = [None]
+        for i in range(n):
+            spec = specs[i]
+            x = xs[i]
+            weight, bias = ctx.params[i][0], ctx.params[i][1]
+            dres, gret, bret = dress[i]
+            link = spec.res_link
+            if dres is not None and link is not None:
+                if link.buf is None:
+                    link.buf = dres
+                else:
+                    link.buf.add_(dres)
+                dres = link.finish()
+            dx, wret, bret_conv = _conv_bwd(x, weight, bias, drs[i], spec, need[1 + 6 * i],
+                                            need[1 + 6 * i + 1], need[1 + 6 * i + 2])
+            grads += [dx, wret, bret_conv, gret, bret, dres]
+        return tuple(grads)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _aligned_copy(t):
+    out = new_act(tuple(t.shape), t)
+    tp, ta = act_of(t)
+    op, oa = act_of(out)
+    call("vae2_copy_act", tp, ctypes.byref(ta), op, ctypes.byref(oa), 0.0, stream_ptr())
+    return out
+
+
+def _bn_layer(x, a, o, dy, dres, save, gamma, part, sums_p, countp, count, relu):
+    def d(t):
+        return act_of(t)[1] if t is not None else Act(0, 0, 0, 0, 0)
+    return _lib.BnLayer(_p(x), d(x), _p(a), d(a), _p(o), d(o), _p(dy), d(dy), _p(dres), d(dres),
+                        _p(save), _p(gamma), _p(part), sums_p, countp, float(count), int(relu))
+
+
+def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=None):
+    """[conv_bn(xs[i], convs[i], bns[i], relu, residuals[i], ...)] for independent layers,
+    their BatchNorm steps batched into shared launches (training mode)."""
+    n = len(xs)
+    residuals = residuals if residuals is not None else [None] * n
+    x_links = x_links if x_links is not None else [None] * n
+    res_links = res_links if res_links is not None else [None] * n
+    relus = relu if isinstance(relu, (list, tuple)) else [relu] * n
+    specs = []
+    for i in range(n):
+        spec = ConvSpec(convs[i], bns[i], relus[i])
+        spec.x_link, spec.res_link = x_links[i], res_links[i]
+        specs.append(spec)
+    if (not all(sp.training for sp in specs) or
+            not all(r is None or _bn_quad_ok(r) for r in residuals)):
+        return [conv_bn(xs[i], convs[i], bns[i], relus[i], residuals[i], x_links[i],
+                        res_links[i]) for i in range(n)]
+    flat = []
+    for i in range(n):
+        flat += [xs[i], convs[i].weight, convs[i].bias, bns[i].weight, bns[i].bias, residuals[i]]
+    return list(_ConvBNMulti.apply(tuple(specs), *flat))
 
 
 class _Conv(torch.autograd.Function):

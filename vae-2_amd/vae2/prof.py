@@ -1,11 +1,22 @@
-"""Live per-kernel timing with HIP events (for bench.py's roofline figure).
+"""Live per-kernel timing with HIP events (bench.py's roofline and per-family table).
 
-A KernelTimer brackets every vae2_conv2d_fwd launch that uses one kernel
-instantiation (by name, as rocprof reports it) with torch.cuda.Events recorded on
-the stream the kernel is launched on, and accumulates the launch's algorithmic
-FLOPs (2 * output pixels * Cout * Cin * k^2).
+StepProfiler brackets every C-ABI call of libvae2_hip with torch.cuda.Events on the
+stream the call launches on, and attributes the span to the kernels the call
+launched (the library's launch log, vae2_kernel_log: names as rocprofv3 reports
+them).  Each timed call is isolated from the side streams (they are waited for
+before it and wait for it after), so an event span is the kernels' own execution,
+as rocprof measures it, not time queued behind a concurrent stream.  The ops
+annotate the calls they make with algorithmic work (note()): FLOPs for the convs,
+bytes moved once for the memory-bound kernels, and a layer-shape label.
+
+Algorithmic FLOPs of a conv: 2 * output pixels * Cout * Cin * k^2 (forward, data
+gradient and weight gradient alike; the data gradient of a stride-2 conv counts
+the same MACs).  Algorithmic bytes: every input read once, every output written
+once (weights included for convs).
 """
 import ctypes
+import re
+from collections import defaultdict
 
 import torch
 
@@ -13,9 +24,44 @@ from . import _lib
 
 _ACTIVE = None
 
+# (family, regex on a kernel name), first match wins (also used by tools/trace_steps.py)
+FAMILIES = (
+    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false>|igemm_kernel<\d+, \d+, \w+, 0"),
+    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true>|igemm_kernel<\d+, \d+, \w+, [12]"),
+    ("conv_wgrad", r"wgrad"),
+    ("batchnorm", r"bn_|reduce_then|chan_partials|partials_reduce"),
+    ("heads", r"upsum|head_|up_adj"),
+    ("fuse_resample", r"upsample|fuse_sum|relu_bwd|copy_act|tile_kernel|spatial_|codemap"),
+    ("optimizer", r"adam|pack_weight"),
+    ("loss_elbo", r"l1_|reparam|weighted_sum|finish_sum|scale_kernel|nonfinite|nchw|nhwc|"
+                  r"sqdiff"),
+    ("torch_aten", r"at::native|^at::"),
+    ("copies", r"rocclr_copy|rocclr_fill"),
+)
+
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E
+
+
+def family(kernel):
+    for f, rx in FAMILIES:
+        if re.search(rx, kernel):
+            return f
+    return "other"
+
 
 def active():
     return _ACTIVE
+
+
+def note(flops=0.0, nbytes=0.0, shape=None):
+    """Annotate the next C-ABI call with its algorithmic work (no-op unless profiling)."""
+    if _ACTIVE is not None:
+        _ACTIVE.pending = (float(flops), float(nbytes), shape)
+
+
+def conv_label(kind, cin, cout, k, stride, h, w):
+    return f"{kind} {cin}->{cout} k{k} s{stride} @{h}x{w}"
 
 
 def fwd_kernel_name(xa, yshape, k, stride, pad):
@@ -29,62 +75,113 @@ def fwd_kernel_name(xa, yshape, k, stride, pad):
     return buf.value.decode()
 
 
-class KernelTimer:
-    def __init__(self, kernel_name):
-        self.kernel_name = kernel_name
-        self.events = []
-        self.flops = []
-        self.bytes = []
-        self.enabled = False
-        self._names = {}
+class StepProfiler:
+    def __init__(self):
+        self.records = []  # (abi fn, kernels label, start ev, end ev, flops, bytes, shape)
+        self.pending = None
+        self._buf = ctypes.create_string_buffer(1 << 14)
 
     def __enter__(self):
         global _ACTIVE
         _ACTIVE = self
-        self.enabled = True
+        _lib.load().vae2_kernel_log(1)
+        _lib.CALL_HOOK = self._call
         return self
 
     def __exit__(self, *exc):
         global _ACTIVE
         _ACTIVE = None
-        self.enabled = False
+        _lib.CALL_HOOK = None
+        _lib.load().vae2_kernel_log(0)
 
-    def matches(self, xa, yshape, spec):
-        key = (xa.n, xa.h, xa.w, xa.c, xa.ps, yshape, spec.k, spec.stride, spec.pad)
-        if key not in self._names:
-            self._names[key] = fwd_kernel_name(xa, yshape, spec.k, spec.stride, spec.pad)
-        return self._names[key] == self.kernel_name
-
-    def record(self, flops, nbytes=0.0):
-        """Start timing one launch on the current stream.  The launch is isolated
-        from the side streams (they are waited for before it, and wait for it
-        after) so the event span is the kernel's own execution, as rocprof sees it,
-        not time spent queued behind a concurrent stream."""
+    def _call(self, name, fn, args):
         from . import streams
+        lib = _lib.load()
         streams.join_all()
-        self.bytes.append(nbytes)
+        cur = torch.cuda.current_stream()
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
-        s.record(torch.cuda.current_stream())
-        self.events.append((s, e))
-        self.flops.append(flops)
-        return e
-
-    @staticmethod
-    def finish(ev):
-        from . import streams
-        cur = torch.cuda.current_stream()
-        ev.record(cur)
+        lib.vae2_kernel_log_read(None, 0)  # drop launches made outside annotated calls
+        s.record(cur)
+        rc = fn(*args)
+        e.record(cur)
         streams.fence_side(cur)
+        n = lib.vae2_kernel_log_read(self._buf, len(self._buf))
+        work = self.pending or (0.0, 0.0, None)
+        self.pending = None
+        if n > 0:
+            self.records.append((name, self._buf.value.decode(), s, e) + work)
+        return rc
 
-    def summary(self):
+    def summary(self, steps):
+        """Per kernel (as rocprof names it), per family and per conv layer shape:
+        time per step, launches per step, algorithmic FLOPs / bytes and the rates."""
         torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e in self.events]
-        n = len(ms)
-        if n == 0:
+        ker = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
+        fam = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
+        shp = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
+        total = 0.0
+        for name, kernels, s, e, flops, nbytes, shape in self.records:
+            ms = s.elapsed_time(e)
+            total += ms
+            ks = kernels.split(";")
+            for d, key in ((ker, kernels), (fam, family(ks[0]))):
+                d[key][0] += ms
+                d[key][1] += 1
+                d[key][2] += flops
+                d[key][3] += nbytes
+            if shape is not None:
+                d = shp[shape]
+                d[0] += ms
+                d[1] += 1
+                d[2] += flops
+                d[3] += nbytes
+
+        def rows(d):
+            out = []
+            for k, (ms, n, fl, by) in sorted(d.items(), key=lambda kv: -kv[1][0]):
+                r = {"name": k, "ms_per_step": round(ms / steps, 4),
+                     "launches_per_step": round(n / steps, 2),
+                     "avg_us": round(1e3 * ms / max(n, 1), 2)}
+                if fl:
+                    r["gflop_per_step"] = round(fl / steps / 1e9, 3)
+                    r["tflops"] = round(fl / (ms * 1e-3) / 1e12, 2)
+                    r["frac_fp32_peak"] = round(fl / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4)
+                if by:
+                    r["gb_per_step"] = round(by / steps / 1e9, 3)
+                    r["gbs"] = round(by / (ms * 1e-3) / 1e9, 1)
+                    r["frac_hbm_peak"] = round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                out.append(r)
+            return out
+
+        return {"kernel_ms_per_step": round(total / steps, 3), "families": rows(fam),
+                "kernels": rows(ker), "conv_shapes": rows(shp)}
+
+    def dominant(self, steps):
+        """The single kernel (one instantiation) with the most time: its launches'
+        average duration and algorithmic work per launch (the roofline object)."""
+        torch.cuda.synchronize()
+        agg = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
+        for name, kernels, s, e, flops, nbytes, shape in self.records:
+            if ";" in kernels:
+                continue
+            a = agg[kernels]
+            a[0] += s.elapsed_time(e)
+            a[1] += 1
+            a[2] += flops
+            a[3] += nbytes
+        if not agg:
             return None
-        tot_ms = sum(ms)
-        return {"launches": n, "avg_us": 1e3 * tot_ms / n,
-                "flops_per_launch": sum(self.flops) / n,
-                "bytes_per_launch": sum(self.bytes) / n,
-                "tflops": sum(self.flops) / (tot_ms * 1e-3) / 1e12}
+        k, (ms, n, fl, by) = max(agg.items(), key=lambda kv: kv[1][0])
+        avg_s = ms * 1e-3 / n
+        out = {"kernel": k, "launches": n, "avg_launch_us": round(avg_s * 1e6, 2),
+               "ms_per_step": round(ms / steps, 3), "flops_per_launch": fl / n,
+               "algorithmic_bytes_per_launch": by / n}
+        if fl > 0:
+            out.update(bound="mfma", achieved=round(fl / n / avg_s / 1e12, 3),
+                       peak=FP32_MFMA_PEAK_TF, unit="TFLOP/s")
+        else:
+            out.update(bound="hbm", achieved=round(by / n / avg_s / 1e9, 1),
+                       peak=HBM_PEAK_GBS, unit="GB/s")
+        out["frac"] = round(out["achieved"] / out["peak"], 4)
+        return out
