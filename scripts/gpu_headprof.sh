@@ -16,7 +16,7 @@ for r in csv.DictReader(open(f)):
 EOF
 pass() {
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "upsum|up_adj|head_out" -f csv \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "upsum|head_|up_adj" -f csv \
     -d gpurun_out/${TAG}_pmc_$name -o run -- python vae-2_amd/tools/head_bench.py --iters 2 \
     > gpurun_out/${TAG}_pmc_$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"

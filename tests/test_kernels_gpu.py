@@ -124,6 +124,54 @@ def ctypes_name(x, yshape):
     return prof.fwd_kernel_name(xa, yshape, 3, 1, 1)
 
 
+def test_multi_bn_equals_per_layer():
+    """conv_bn_multi (independent layers of one depth level sharing every BatchNorm
+    launch) == the same layers one by one, bit for bit: outputs, input / residual /
+    parameter gradients and running statistics."""
+    from vae2 import ops
+    torch.manual_seed(6)
+    shapes = [(2, 16, 32, 18, 18), (2, 8, 16, 36, 36), (2, 4, 8, 72, 72), (2, 2, 4, 144, 144),
+              (2, 16, 32, 18, 36), (2, 8, 16, 36, 72), (2, 4, 8, 72, 144)]  # 7 > 6: two launches
+
+    def make(seed):
+        torch.manual_seed(seed)
+        layers = []
+        for n, h, w, ci, co in shapes:
+            conv = nn.Conv2d(ci, co, 3, 1, 1, bias=False).to(DEV)
+            bn = nn.BatchNorm2d(co, momentum=0.01).to(DEV)
+            nn.init.normal_(bn.weight, 1.0, 0.2)
+            nn.init.normal_(bn.bias, 0.0, 0.2)
+            layers.append((conv, bn))
+        xs = [ops.new_act((n, h, w, ci), torch.empty(1, device=DEV)) for n, h, w, ci, co in shapes]
+        rs = [ops.new_act((n, h, w, co), xs[0]) for n, h, w, ci, co in shapes]
+        for t in xs + rs:
+            with torch.no_grad():
+                t.normal_()
+            t.requires_grad_(True)
+        return layers, xs, rs
+
+    la, xa, ra = make(7)
+    lb, xb, rb = make(7)
+    ya = ops.conv_bn_multi(xa, [c for c, _ in la], [b for _, b in la], True,
+                           residuals=[r if i % 2 else None for i, r in enumerate(ra)])
+    yb = [ops.conv_bn(x, c, b, True, r if i % 2 else None)
+          for i, ((c, b), x, r) in enumerate(zip(lb, xb, rb))]
+    gs = [torch.randn_like(y) for y in ya]
+    torch.autograd.backward(ya, gs)
+    torch.autograd.backward(yb, gs)
+    torch.cuda.synchronize()
+    for u, v in zip(ya, yb):
+        assert torch.equal(u, v)
+    for u, v in zip(xa + [r for i, r in enumerate(ra) if i % 2],
+                    xb + [r for i, r in enumerate(rb) if i % 2]):
+        assert torch.equal(u.grad, v.grad)
+    for (ca, ba), (cb, bb) in zip(la, lb):
+        for p, q in ((ca.weight, cb.weight), (ba.weight, bb.weight), (ba.bias, bb.bias)):
+            assert torch.equal(p.grad, q.grad)
+        assert torch.equal(ba.running_mean, bb.running_mean)
+        assert torch.equal(ba.running_var, bb.running_var)
+
+
 @pytest.mark.parametrize("cin,cout,h,w", [(18, 18, 16, 32), (64, 36, 12, 40)])
 def test_direct_conv3x3_bn_stats(cin, cout, h, w):
     """BN statistics from the direct kernel's epilogue (its own partial-row count)."""
