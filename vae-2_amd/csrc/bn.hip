@@ -97,7 +97,6 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
 // load/store of a contiguous pixel run.  Needs pixel strides % 4 == 0, 16-byte
 // aligned bases and ceil(C/4) <= 256.  Channels >= C of the last quad are read
 // (pixel padding, discarded) but never written.
-typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 

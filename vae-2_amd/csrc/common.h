@@ -31,6 +31,33 @@ void note_kernel(const void* host_fn);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------- range-checked loads ----
+// A raw buffer load whose byte offset is >= the descriptor's num_records returns 0.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  uint64_t b = (uint64_t)base;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* pb = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+__device__ __forceinline__ void store1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+
 // ------------------------------------------------------- activations ----
 // Device-side copy of vae2_act with 32-bit-safe strides kept in 64-bit.
 struct Act {

@@ -25,22 +25,8 @@
 
 namespace vae2 {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
-
-// ------------------------------------------------- range-checked loads ----
-// A raw buffer load whose byte offset is >= the descriptor's num_records returns 0.
-constexpr uint32_t kOOB = 0x80000000u;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  uint64_t b = (uint64_t)base;
-  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  void* pb = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
 
 // Bijective blockIdx remap (T1): blocks are dealt round-robin over the 8 XCDs, so
 // logical tiles are re-numbered to make each XCD own a contiguous run of tiles
@@ -50,13 +36,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
   return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (orig >> 3);
 }
 
-__device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-__device__ __forceinline__ float load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
 
 // ------------------------------------------------------------ weight pack ----
 // mode 0: out[n][t][c4] = w[n][c][t]         n < round_up(cout,64), c4 < round_up(cin,4)

@@ -17,7 +17,6 @@
 
 namespace vae2 {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kHeadMaxOut = 4;
 
@@ -127,27 +126,39 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
     float db[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) { dw[o] = s0; db[o] = 0.f; }
-    for (int64_t p = p0 + r; p < p1; p += rows) {
-      const f4 v = hld4(yb_at(y, P, p, c));
-      float d[CO];
+    constexpr int U = 4;  // pixels in flight per thread
+    for (int64_t pb = p0 + r; pb < p1; pb += U * rows) {
+      f4 vv[U];
+      float dd[U][CO];
 #pragma unroll
-      for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = pb + u * rows;
+        const bool ok = p < p1;
+        vv[u] = ok ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
-        const bool m = h > 0.f;
-        h = m ? h : 0.f;
-        float dh = 0.f;
-#pragma unroll
-        for (int o = 0; o < CO; ++o) dh += wv[o][k] * d[o];
-        const float g = m ? dh : 0.f;
-        s0[k] += g;
-        s1[k] += g * (v[k] - hc.mean[k]) * hc.invstd[k];
-#pragma unroll
-        for (int o = 0; o < CO; ++o) dw[o][k] += d[o] * h;
+        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? dout[p * dod.ps + o] : 0.f;
       }
 #pragma unroll
-      for (int o = 0; o < CO; ++o) db[o] += d[o];
+      for (int u = 0; u < U; ++u) {
+        const f4 v = vv[u];
+        const float* d = dd[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
+          const bool m = h > 0.f;
+          h = m ? h : 0.f;
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) dh += wv[o][k] * d[o];
+          const float g = m ? dh : 0.f;
+          s0[k] += g;
+          s1[k] += g * (v[k] - hc.mean[k]) * hc.invstd[k];
+#pragma unroll
+          for (int o = 0; o < CO; ++o) dw[o][k] += d[o] * h;
+        }
+#pragma unroll
+        for (int o = 0; o < CO; ++o) db[o] += d[o];
+      }
     }
     float* rr = red + r * NC;
 #pragma unroll
@@ -171,22 +182,33 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
   }
 }
 
-// Column sums of the reduce partials (coalesced: lane = column, 4 waves over rows in
-// double, combined in a fixed order) routed to their destinations.
-__global__ __launch_bounds__(256) void head_bwd_colsum_kernel(
+// Column sums of the reduce partials (lane = column; 16 waves over rows with four
+// independent accumulators each, in double; combined in a fixed order) routed to their
+// destinations.
+__global__ __launch_bounds__(1024) void head_bwd_colsum_kernel(
     const float* __restrict__ part, int nrows, int C, int CO, double* __restrict__ sums,
     float* dgamma, float* dbeta, float* dw2, float* db2) {
-  __shared__ double red[4][64];
+  __shared__ double red[16][64];
   const int NC = 2 * C + CO * C + CO;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
-  double s = 0.0;
-  if (col < NC)
-    for (int i = wave; i < nrows; i += 4) s += (double)part[(int64_t)i * NC + col];
-  red[wave][lane] = s;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (col < NC) {
+    int i = wave;
+    for (; i + 48 < nrows; i += 64) {
+      s0 += (double)part[(int64_t)i * NC + col];
+      s1 += (double)part[(int64_t)(i + 16) * NC + col];
+      s2 += (double)part[(int64_t)(i + 32) * NC + col];
+      s3 += (double)part[(int64_t)(i + 48) * NC + col];
+    }
+    for (; i < nrows; i += 16) s0 += (double)part[(int64_t)i * NC + col];
+  }
+  red[wave][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wave != 0 || col >= NC) return;
-  s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) s += red[w][lane];
   if (col < C) {
     sums[col] = s;
     if (dbeta) dbeta[col] += (float)s;
@@ -229,30 +251,43 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
       k4[k] = (gamma ? gamma[ch] : 1.f) * hc.invstd[k];
     }
     f4 sdy = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t p = p0 + r; p < p1; p += rows) {
-      const f4 v = hld4(yb_at(y, P, p, c));
-      float d[CO];
+    constexpr int U = 4;  // pixels in flight per thread
+    for (int64_t pb = p0 + r; pb < p1; pb += U * rows) {
+      f4 vv[U];
+      float dd[U][CO];
 #pragma unroll
-      for (int o = 0; o < CO; ++o) d[o] = dout[p * dod.ps + o];
-      f4 o4;
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = pb + u * rows;
+        const bool ok = p < p1;
+        vv[u] = ok ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
-        float dh = 0.f;
-#pragma unroll
-        for (int o = 0; o < CO; ++o) dh += wv[o][k] * d[o];
-        const float g = h > 0.f ? dh : 0.f;
-        const float xh = (v[k] - hc.mean[k]) * hc.invstd[k];
-        o4[k] = k4[k] * (g - mg[k] - xh * mgx[k]);
-        sdy[k] += o4[k];
+        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? dout[p * dod.ps + o] : 0.f;
       }
-      float* dst = dy + p * dyd.ps + c;
-      if (c + 4 <= C) {
-        *reinterpret_cast<f4*>(dst) = o4;
-      } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (c + k < C) dst[k] = o4[k];
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = pb + u * rows;
+        if (p >= p1) break;
+        const f4 v = vv[u];
+        f4 o4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float h = __builtin_fmaf(v[k], hc.sc[k], hc.sh[k]);
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) dh += wv[o][k] * dd[u][o];
+          const float g = h > 0.f ? dh : 0.f;
+          const float xh = (v[k] - hc.mean[k]) * hc.invstd[k];
+          o4[k] = k4[k] * (g - mg[k] - xh * mgx[k]);
+          sdy[k] += o4[k];
+        }
+        float* dst = dy + p * dyd.ps + c;
+        if (c + 4 <= C) {
+          *reinterpret_cast<f4*>(dst) = o4;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (c + k < C) dst[k] = o4[k];
+        }
       }
     }
 #pragma unroll
@@ -270,27 +305,34 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
 // ------------------------------------------------------------------ up-sum ----
 // y[n,oy,x,c] = sum_k x0[n,oy,x,k] W0[c][k] + sum_s up(z_s)[n,oy,x,c] + bias[c]
 // (the wide head conv split by branch; z_s = W_s y_s at the branch resolution).
-// Workgroup = (image row, 64-pixel chunk, 64-channel block); wave w owns pixels
-// 16w..16w+15.  The full-resolution block W0 x0 (K = Cin0 <= 32) is a 16x64 MFMA tile
-// per wave (v_mfma_f32_16x16x4f32, packed W0, fragments straight from global/L2).  Each
-// source's two contributing rows are blended vertically once into LDS (batched loads,
-// one memory round trip) with per-pixel horizontal tables; the epilogue adds the two
-// horizontal taps per source, the bias, writes y and the BN partial sums.
+// Workgroup = (band of kUsRows image rows, 64-pixel chunk, 64-channel block); wave w
+// owns pixels 16w..16w+15 of each row.  The W0 fragments and the horizontal
+// interpolation tables are set up once per workgroup; per row the full-resolution block
+// W0 x0 (K = Cin0 <= 32) is a 16x64 MFMA tile per wave (v_mfma_f32_16x16x4f32), each
+// source's two contributing rows are blended vertically into LDS (one batch of
+// unconditional buffer loads, source columns clamped into the chunk's window), and the
+// epilogue adds the two horizontal taps per source and the bias, stores y and
+// accumulates the BN partial sums (written once per workgroup).
 constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32, kUsVS = 68;  // VS: LDS column stride
+constexpr int kUsRows = 8;                                          // image rows per workgroup
 
 struct UpSum {
   const float* x;
   int x_ps, cin, cin4, H, W;
+  uint32_t x_bytes;
   const float* wp;  // packed [round_up(C,64)][cin4]
+  uint32_t wp_bytes;
   const float* bias;
   const float* z[3];
+  uint32_t z_bytes[3];
   int zh[3], zw[3], zps[3];
   float sh[3], sw[3];
   int vcols[3];  // staged source columns per 64-pixel chunk
   float* y;
-  int y_ps, C;
-  float* stats;  // [2][rows][C], row = (n*H + oy)*nxb + xb
-  int rows, nxb;
+  uint32_t y_bytes;
+  int C;
+  float* stats;  // [2][rows][C], row = (n*nrb + band)*nxb + xb
+  int rows, nxb, nrb;
 };
 
 template <int NUP>
@@ -299,53 +341,39 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   __shared__ float red[2][4][kUsCB];
   f4* tab = reinterpret_cast<f4*>(usm);                  // [NUP][kUsXB] {i0, i1, l0, l1}
   float* vs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [sum_s vcols_s][kUsVS]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r = lane & 15;
-  // block order: chunk fastest, then channel block, then image row, so the workgroups
-  // in flight cover a few consecutive rows (page / L2 locality of the NHWC rows)
+  // block order: chunk fastest, then channel block, then row band
   const int ncb = (p.C + kUsCB - 1) / kUsCB;
   const int xb = blockIdx.x % p.nxb, x0 = xb * kUsXB;
   const int cbi = (blockIdx.x / p.nxb) % ncb;
-  const int row = blockIdx.x / (p.nxb * ncb);
-  const int n = row / p.H, oy = row - n * p.H;
+  const int band = blockIdx.x / (p.nxb * ncb);
+  const int n = band / p.nrb, oy0 = (band - n * p.nrb) * kUsRows;
+  const int ny = p.H - oy0 < kUsRows ? p.H - oy0 : kUsRows;
   const int c0 = cbi * kUsCB;
   const int xn = p.W - x0 < kUsXB ? p.W - x0 : kUsXB;
-  // ---- MFMA operands (issued first: their latency overlaps the staging below) ----
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.wp, p.wp_bytes);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, p.y_bytes);
+  // ---- W0 fragments (once) ----
   const int kq = p.cin4 >> 2;
-  const float* xrow = p.x + ((int64_t)row * p.W + x0) * p.x_ps;
-  const int pxa = 16 * wave + r;
-  float fa[kUsMaxCin / 4], fb[kUsMaxCin / 4][4];
+  float fb[kUsMaxCin / 4][4];
 #pragma unroll
-  for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
-    const int k = 4 * kb + g;
-    fa[kb] = (kb < kq && pxa < xn && k < p.cin) ? xrow[(int64_t)pxa * p.x_ps + k] : 0.f;
+  for (int kb = 0; kb < kUsMaxCin / 4; ++kb)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      fb[kb][j] = (kb < kq) ? p.wp[(int64_t)(c0 + 16 * j + r) * p.cin4 + k] : 0.f;
-  }
-  // ---- vertical blends of each source over the chunk's source-column window ----
-  constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
+      fb[kb][j] = load1(wr, kb < kq ? (uint32_t)((c0 + 16 * j + r) * p.cin4 + 4 * kb + g) * 4u
+                                    : kOOB);
+  // ---- horizontal tables and source windows (once) ----
   const int c = c0 + lane;
   const bool cok = c < p.C;
-  float a0[NUP > 0 ? NUP : 1][VU], a1[NUP > 0 ? NUP : 1][VU];
   int vlo[3] = {0, 0, 0}, vhi[3] = {0, 0, 0}, voff[3] = {0, 0, 0};
-  Lerp ly[3];
 #pragma unroll
   for (int s = 0; s < NUP; ++s) {
     vlo[s] = lerp_index(x0, p.zw[s], p.sw[s]).i0;
     vhi[s] = lerp_index(x0 + xn - 1, p.zw[s], p.sw[s]).i1;
     voff[s] = s == 0 ? 0 : voff[s - 1] + p.vcols[s - 1];
-    ly[s] = lerp_index(oy, p.zh[s], p.sh[s]);
-    const int64_t ibase = (int64_t)n * p.zh[s];
-    const float* r0 = p.z[s] + (ibase + ly[s].i0) * p.zw[s] * p.zps[s] + c;
-    const float* r1 = p.z[s] + (ibase + ly[s].i1) * p.zw[s] * p.zps[s] + c;
-#pragma unroll
-    for (int u = 0; u < VU; ++u) {
-      const int ix = vlo[s] + wave + 4 * u;
-      const bool ok = cok && ix <= vhi[s];
-      a0[s][u] = ok ? r0[(int64_t)ix * p.zps[s]] : 0.f;
-      a1[s][u] = ok ? r1[(int64_t)ix * p.zps[s]] : 0.f;
-    }
     if (threadIdx.x < xn) {
       const Lerp lx = lerp_index(x0 + threadIdx.x, p.zw[s], p.sw[s]);
       tab[s * kUsXB + threadIdx.x] =
@@ -353,29 +381,6 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
              __int_as_float((voff[s] + lx.i1 - vlo[s]) * kUsVS), lx.l0, lx.l1};
     }
   }
-#pragma unroll
-  for (int s = 0; s < NUP; ++s) {
-#pragma unroll
-    for (int u = 0; u < VU; ++u) {
-      const int ix = vlo[s] + wave + 4 * u;
-      if (ix <= vhi[s])
-        vs[(voff[s] + ix - vlo[s]) * kUsVS + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
-    }
-  }
-  // ---- W0 x0: acc[j][e] = pixel 16*wave + 4g + e, channel c0 + 16j + r ----
-  f4 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
-    if (kb < kq) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kb], fb[kb][j], acc[j], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-  // ---- epilogue ----
   float bj[4], s1[4], s2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -384,28 +389,79 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
     s1[j] = 0.f;
     s2[j] = 0.f;
   }
-  const int64_t P = (int64_t)(p.rows / p.nxb) * p.W;
-  float* ybase = p.y + (int64_t)cbi * P * 64 + ((int64_t)row * p.W + x0) * 64 + r;
+  const int64_t P = (int64_t)(p.rows / p.nxb / p.nrb) * p.H * p.W;  // n * H * W
+  constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
+  const int pxa = 16 * wave + r;
+  for (int ry = 0; ry < ny; ++ry) {
+    const int oy = oy0 + ry, row = n * p.H + oy;
+    // ---- loads: x0 fragments and the two source rows of every source ----
+    float fa[kUsMaxCin / 4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int px = 16 * wave + 4 * g + e;
-    if (px >= xn) continue;
-    f4 t[3];
+    for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+      const int k = 4 * kb + g;
+      fa[kb] = load1(xr, (kb < kq && pxa < xn && k < p.cin)
+                             ? (uint32_t)(((row * p.W + x0 + pxa) * p.x_ps + k) * 4u) : kOOB);
+    }
+    float a0[NUP > 0 ? NUP : 1][VU], a1[NUP > 0 ? NUP : 1][VU];
+    Lerp ly[3];
 #pragma unroll
-    for (int s = 0; s < NUP; ++s) t[s] = tab[s * kUsXB + px];
+    for (int s = 0; s < NUP; ++s) {
+      ly[s] = lerp_index(oy, p.zh[s], p.sh[s]);
+      const __amdgpu_buffer_rsrc_t zr = make_rsrc(p.z[s], p.z_bytes[s]);
+      const int rb0 = ((n * p.zh[s] + ly[s].i0) * p.zw[s]) * p.zps[s] + c;
+      const int rb1 = ((n * p.zh[s] + ly[s].i1) * p.zw[s]) * p.zps[s] + c;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = acc[j][e];
-#pragma unroll
-      for (int s = 0; s < NUP; ++s) {
-        const float* vj = vs + 16 * j + r;
-        v += t[s][2] * vj[__float_as_int(t[s][0])] + t[s][3] * vj[__float_as_int(t[s][1])];
+      for (int u = 0; u < VU; ++u) {
+        int ix = vlo[s] + wave + 4 * u;
+        ix = ix < vhi[s] ? ix : vhi[s];
+        a0[s][u] = load1(zr, cok ? (uint32_t)(rb0 + ix * p.zps[s]) * 4u : kOOB);
+        a1[s][u] = load1(zr, cok ? (uint32_t)(rb1 + ix * p.zps[s]) * 4u : kOOB);
       }
-      v += bj[j];
-      if (c0 + 16 * j + r < p.C) {
-        ybase[(int64_t)px * 64 + 16 * j] = v;
-        s1[j] += v;
-        s2[j] += v * v;
+    }
+    __syncthreads();  // the previous row's epilogue reads of vs are done (and tab is written)
+#pragma unroll
+    for (int s = 0; s < NUP; ++s) {
+#pragma unroll
+      for (int u = 0; u < VU; ++u) {
+        const int j = wave + 4 * u;  // uniform per wave
+        if (vlo[s] + j <= vhi[s])
+          vs[(voff[s] + j) * kUsVS + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
+      }
+    }
+    // ---- W0 x0: acc[j][e] = pixel 16*wave + 4g + e, channel c0 + 16j + r ----
+    f4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+      if (kb < kq) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kb], fb[kb][j], acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    // ---- epilogue ----
+    const uint32_t ybase = (uint32_t)(cbi * P * 64 + ((int64_t)row * p.W + x0) * 64 + r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int px = 16 * wave + 4 * g + e;
+      f4 t[3];
+#pragma unroll
+      for (int s = 0; s < NUP; ++s) t[s] = tab[s * kUsXB + (px < xn ? px : xn - 1)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[j][e];
+#pragma unroll
+        for (int s = 0; s < NUP; ++s) {
+          const float* vj = vs + 16 * j + r;
+          v += t[s][2] * vj[__float_as_int(t[s][0])] + t[s][3] * vj[__float_as_int(t[s][1])];
+        }
+        v += bj[j];
+        const bool ok = px < xn && c0 + 16 * j + r < p.C;
+        store1(yr, ok ? (ybase + px * 64 + 16 * j) * 4u : kOOB, v);
+        s1[j] += ok ? v : 0.f;
+        s2[j] += ok ? v * v : 0.f;
       }
     }
   }
@@ -426,7 +482,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
     }
     __syncthreads();
     if (wave == 0 && cok) {
-      const int rr = row * p.nxb + xb;
+      const int rr = (n * p.nrb + oy0 / kUsRows) * p.nxb + xb;
       p.stats[(int64_t)rr * p.C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] +
                                        red[0][3][lane];
       p.stats[((int64_t)p.rows + rr) * p.C + c] = red[1][0][lane] + red[1][1][lane] +
@@ -671,7 +727,7 @@ int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* sa
                 as_stream(stream), y, to_act(yd), save, w2, dout, to_act(doutd), ppb, rows, ws);
   int rc = check_launch(fn);
   if (rc) return rc;
-  VAE2_LAUNCH(head_bwd_colsum_kernel, dim3((unsigned)ceil_div(NC, 64)), dim3(256), 0,
+  VAE2_LAUNCH(head_bwd_colsum_kernel, dim3((unsigned)ceil_div(NC, 64)), dim3(1024), 0,
                      as_stream(stream), (const float*)ws, (int)blocks, C, cout2, sums, dgamma,
                      dbeta, dw2, db2);
   return check_launch(fn);
@@ -705,7 +761,7 @@ int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* sav
 
 int64_t vae2_conv1x1_upsum_stats_rows(const vae2_act* yd) {
   if (!act_ok(yd)) return 0;
-  return yd->n * yd->h * ceil_div(yd->w, kUsXB);
+  return yd->n * ceil_div(yd->h, kUsRows) * ceil_div(yd->w, kUsXB);
 }
 
 int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
@@ -721,26 +777,38 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   p.x = x; p.x_ps = (int)xd->ps; p.cin = (int)xd->c; p.cin4 = ((int)xd->c + 3) / 4 * 4;
   p.H = (int)yd->h; p.W = (int)yd->w;
   p.wp = wp; p.bias = bias;
+  const int64_t P = act_pixels(yd);
+  const int64_t ncb = ceil_div(yd->c, kUsCB);
+  const int64_t x_bytes = act_pixels(xd) * xd->ps * 4;
+  const int64_t y_bytes = ncb * P * 64 * 4;
+  VAE2_REQUIRE(x_bytes < (1ll << 31) && y_bytes < (1ll << 31), fn,
+               "tensor too large for 32-bit offsets");
+  p.x_bytes = (uint32_t)x_bytes;
+  p.wp_bytes = (uint32_t)(ncb * kUsCB * p.cin4 * 4);
   int vtot = 0;
   for (int s = 0; s < nup; ++s) {
     const vae2_act* u = &upds[s];
     VAE2_REQUIRE(ups[s] && act_ok(u) && u->n == yd->n && u->c >= yd->c && u->h <= yd->h &&
                      u->w <= yd->w, fn, "up-sum term shape mismatch");
+    const int64_t zb = act_pixels(u) * u->ps * 4;
+    VAE2_REQUIRE(zb < (1ll << 31), fn, "up-sum term too large for 32-bit offsets");
     p.z[s] = ups[s]; p.zh[s] = (int)u->h; p.zw[s] = (int)u->w; p.zps[s] = (int)u->ps;
+    p.z_bytes[s] = (uint32_t)zb;
     p.sh[s] = (float)u->h / (float)yd->h;
     p.sw[s] = (float)u->w / (float)yd->w;
     p.vcols[s] = (int)ceilf(p.sw[s] * kUsXB) + 3;
     VAE2_REQUIRE(p.vcols[s] <= 48, fn, "source wider than half the output (upsampling only)");
     vtot += p.vcols[s];
   }
-  p.y = y; p.y_ps = (int)yd->ps; p.C = (int)yd->c;
+  p.y = y; p.y_bytes = (uint32_t)y_bytes; p.C = (int)yd->c;
   p.stats = stats;
   p.nxb = (int)ceil_div(yd->w, kUsXB);
+  p.nrb = (int)ceil_div(yd->h, kUsRows);
   p.rows = (int)vae2_conv1x1_upsum_stats_rows(yd);
   const int nu = nup > 0 ? nup : 1;
   const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1) * kUsVS) *
                      sizeof(float);
-  dim3 grid((unsigned)(yd->n * yd->h * p.nxb * ceil_div(yd->c, kUsCB)));
+  dim3 grid((unsigned)(yd->n * p.nrb * p.nxb * ncb));
   hipStream_t st = as_stream(stream);
   switch (nup) {
     case 0: VAE2_LAUNCH(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
