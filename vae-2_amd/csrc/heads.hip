@@ -657,6 +657,122 @@ __global__ __launch_bounds__(256) void up_adj_v_kernel(UpAdj p, int s) {
   }
 }
 
+// Exact 2^(s+1) ratios (the HRNet branches of a power-of-two image): static stencils.
+// Source column i receives the 2F output pixels F*i + d, d = -F/2 .. 3F/2-1, with the hat
+// weight 1 - |2d + 1 - F| / 2F (interpolate's lerp weights, exact in fp32); at the image
+// edges the forward's clamped tap lands on column 0 / zw-1, i.e. the virtual columns -1
+// and zw are folded into them.  Same rule vertically.
+__device__ constexpr float hat_w(int d, int f) {
+  return 1.f - (float)(2 * d + 1 - f < 0 ? f - 1 - 2 * d : 2 * d + 1 - f) / (float)(2 * f);
+}
+
+constexpr int kAdjHalo = 4;  // F/2 for F <= 8
+
+// Horizontal pass, workgroup = (dY row, 64-pixel chunk, 64-channel block); the chunk and a
+// 4-pixel halo are staged in LDS (lane = channel); wave w computes the owned source
+// columns j = w, w + 4, ... of every source with immediate LDS offsets.
+template <int NUP>
+__global__ __launch_bounds__(256) void up_adj2_h_kernel(UpAdj p) {
+  constexpr int SPAN = kUsXB + 2 * kAdjHalo, PER = SPAN / 4;
+  __shared__ float st[SPAN][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncb = (p.C + 63) / 64;
+  const int xb = blockIdx.x % p.nxb;
+  const int cbi = (blockIdx.x / p.nxb) % ncb;
+  const int row = blockIdx.x / (p.nxb * ncb);  // n*H + oy
+  const int c = cbi * 64 + lane;
+  const bool cok = c < p.C;
+  const int x0 = xb * kUsXB;
+  const float* drow = p.dy + (int64_t)row * p.W * p.dy_ps + (cok ? c : 0);
+  float v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int ox = x0 - kAdjHalo + wave + 4 * u;
+    v[u] = (cok && ox >= 0 && ox < p.W) ? drow[(int64_t)ox * p.dy_ps] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) st[wave + 4 * u][lane] = v[u];
+  __syncthreads();
+  if (!cok) return;
+#pragma unroll
+  for (int s = 0; s < NUP; ++s) {
+    const int F = 2 << s, zw = p.zw[s];
+    const float* sw = &st[F * wave + kAdjHalo][lane];  // column j = wave: pixels F*wave + d
+    float* hrow = p.hb[s] + (int64_t)row * zw * p.C + c;
+#pragma unroll
+    for (int jj = 0; jj < kUsXB / (2 << s) / 4; ++jj) {
+      const int j = wave + 4 * jj, ix = x0 / F + j;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -(1 << s); d < 3 * (1 << s); ++d) acc += hat_w(d, F) * sw[(4 * F * jj + d) * 64];
+      if (ix == 0) {  // virtual column -1 (pixels d - F)
+#pragma unroll
+        for (int d = 2 << s; d < 3 * (1 << s); ++d) acc += hat_w(d, F) * sw[(d - F) * 64];
+      }
+      if (ix == zw - 1) {  // virtual column zw (pixels F*(j+1) + d)
+#pragma unroll
+        for (int d = -(1 << s); d < 0; ++d) acc += hat_w(d, F) * sw[(4 * F * jj + F + d) * 64];
+      }
+      hrow[(int64_t)ix * p.C] = acc;
+    }
+  }
+}
+
+// Vertical pass of source S (F = 2^(S+1)), workgroup = (target row, 64-channel block).
+template <int S>
+__global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
+  constexpr int F = 2 << S, HF = 1 << S;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row = blockIdx.x;  // n*zh + iy
+  const int zh = p.zh[S], zw = p.zw[S];
+  const int n = row / zh, iy = row - n * zh;
+  const int c = blockIdx.y * 64 + lane;
+  if (c >= p.C) return;
+  const int64_t rs = (int64_t)zw * p.C;
+  const float* hb = p.hb[S] + (int64_t)n * p.H * rs + c;
+  float* out = p.dx[S] + (int64_t)row * zw * p.dx_ps[S] + c;
+  const int oy0 = F * iy;
+  constexpr int U = 4;  // target columns per wave iteration (their loads in flight together)
+  constexpr int NT = 3 * F;  // 2F taps + the two edge folds (HF rows each)
+  for (int ix0 = wave; ix0 < zw; ix0 += 4 * U) {
+    float v[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ix = ix0 + 4 * u;
+      const float* h = hb + (int64_t)(ix < zw ? ix : zw - 1) * p.C;
+#pragma unroll
+      for (int d = -HF; d < 3 * HF; ++d) {
+        const int oy = oy0 + d;
+        v[u][d + HF] = (oy >= 0 && oy < p.H) ? h[(int64_t)oy * rs] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < HF; ++e) {  // edge folds: rows d - F (top, d = F + e), F*zh + d
+        v[u][2 * F + e] = iy == 0 ? h[(int64_t)e * rs] : 0.f;
+        v[u][2 * F + HF + e] = iy == zh - 1 ? h[(int64_t)(F * zh - HF + e) * rs] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ix = ix0 + 4 * u;
+      if (ix >= zw) break;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -HF; d < 3 * HF; ++d) acc += hat_w(d, F) * v[u][d + HF];
+      if (iy == 0) {
+#pragma unroll
+        for (int e = 0; e < HF; ++e) acc += hat_w(F + e, F) * v[u][2 * F + e];
+      }
+      if (iy == zh - 1) {
+#pragma unroll
+        for (int e = 0; e < HF; ++e) acc += hat_w(e - HF, F) * v[u][2 * F + HF + e];
+      }
+      out[(int64_t)ix * p.dx_ps[S]] = acc;
+    }
+  }
+}
+
 // Pixels per block of the backward passes (<= 1024 blocks, >= 64 pixels each).
 static int64_t head_ppb(int64_t P) {
   int64_t ppb = ceil_div(P, 1024);
@@ -852,15 +968,39 @@ int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n
     p.hb[s] = hb;
     hb += dyd->n * dyd->h * d->w * dyd->c;
   }
-  // halo: the owned columns' windows reach at most 1/sw + 3 pixels past the chunk
-  p.halo = (int)ceilf(1.f / min_sw) + 4;
   p.nxb = (int)ceil_div(dyd->w, kUsXB);
   const unsigned cb = (unsigned)ceil_div(dyd->c, 64);
+  hipStream_t st = as_stream(stream);
+  bool pow2 = dyd->w % kUsXB == 0;
+  for (int s = 0; s < n; ++s)
+    pow2 = pow2 && dyd->w == (int64_t)p.zw[s] << (s + 1) && dyd->h == (int64_t)p.zh[s] << (s + 1);
+  if (pow2) {
+    const dim3 grid((unsigned)(dyd->n * dyd->h * p.nxb * cb));
+    switch (n) {
+      case 1: VAE2_LAUNCH(up_adj2_h_kernel<1>, grid, dim3(256), 0, st, p); break;
+      case 2: VAE2_LAUNCH(up_adj2_h_kernel<2>, grid, dim3(256), 0, st, p); break;
+      default: VAE2_LAUNCH(up_adj2_h_kernel<3>, grid, dim3(256), 0, st, p); break;
+    }
+    int rc = check_launch(fn);
+    if (rc) return rc;
+    for (int s = 0; s < n; ++s) {
+      const dim3 gv((unsigned)(dyd->n * p.zh[s]), cb);
+      switch (s) {
+        case 0: VAE2_LAUNCH(up_adj2_v_kernel<0>, gv, dim3(256), 0, st, p); break;
+        case 1: VAE2_LAUNCH(up_adj2_v_kernel<1>, gv, dim3(256), 0, st, p); break;
+        default: VAE2_LAUNCH(up_adj2_v_kernel<2>, gv, dim3(256), 0, st, p); break;
+      }
+      rc = check_launch(fn);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  // halo: the owned columns' windows reach at most 1/sw + 3 pixels past the chunk
+  p.halo = (int)ceilf(1.f / min_sw) + 4;
   const int span = kUsXB + 2 * p.halo;
   const size_t shm = (size_t)(4 * n + 64) * span * sizeof(float);
   VAE2_REQUIRE(shm <= 64 * 1024, fn, "upsampling ratio too large for the LDS tile");
   dim3 grid((unsigned)(dyd->n * dyd->h * p.nxb * cb));
-  hipStream_t st = as_stream(stream);
   switch (n) {
     case 1: VAE2_LAUNCH(up_adj_h_kernel<1>, grid, dim3(256), shm, st, p); break;
     case 2: VAE2_LAUNCH(up_adj_h_kernel<2>, grid, dim3(256), shm, st, p); break;
