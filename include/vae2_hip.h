@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 4
+#define VAE2_ABI_VERSION 5
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -160,6 +160,20 @@ int vae2_bn_reduce_finalize(const float* partials, int64_t rows, int64_t c,
                             int64_t* num_batches_tracked, float momentum, float eps,
                             float* save, void* stream);
 
+/* The same with shifted statistics: partials / sums hold sums of (x - mean_shift[c])
+ * (vae2_conv1x1_upsum_fwd's, centred on the conv bias so E[x^2] - E[x]^2 does not
+ * cancel); the mean (save, running_mean) gets mean_shift back.  mean_shift may be NULL. */
+int vae2_bn_reduce_finalize_shifted(const float* partials, int64_t rows, int64_t c,
+                                    double* sums, double count, const float* mean_shift,
+                                    const float* gamma, const float* beta,
+                                    float* running_mean, float* running_var,
+                                    int64_t* num_batches_tracked, float momentum, float eps,
+                                    float* save, void* stream);
+int vae2_bn_finalize_shifted(const double* sums, double count, const float* mean_shift,
+                             const float* gamma, const float* beta, float* running_mean,
+                             float* running_var, int64_t* num_batches_tracked, float momentum,
+                             float eps, int64_t c, float* save, void* stream);
+
 /* Backward: partials [2][rows][c] of (sum g, sum g*xhat) -> sums [2][c] (double)
  * and dgamma += sum g*xhat, dbeta += sum g, in one launch.                       */
 int vae2_bn_bwd_reduce_param_grads(const float* partials, int64_t rows, int64_t c,
@@ -257,7 +271,8 @@ int vae2_bn_multi_finalize(int n, const vae2_bn_fin* fins, void* stream);
  * y = conv1x1(x, wp) + bias + sum_s bilinear_up(ups[s]) to y's h, w (align_corners=False;
  * channels [0, yd->c) of each ups[s], nup <= 3), wp = the W0 block packed as
  * vae2_conv2d_pack_weight(_ld) mode 0 (Cin0 <= 32); optional BN partial statistics
- * stats [2][vae2_conv1x1_upsum_stats_rows(yd)][Cout].
+ * stats [2][vae2_conv1x1_upsum_stats_rows(yd)][Cout] of y - bias (shifted: finalize
+ * with vae2_bn_reduce_finalize_shifted / vae2_bn_finalize_shifted, mean_shift = bias).
  * y is written in the 64-channel-blocked layout B64 (not NHWC):
  *     element (p, c) at y[(c / 64) * P * 64 + p * 64 + c % 64],  P = n*h*w,
  * i.e. ceil(Cout/64) * P * 64 floats (yd->ps is ignored).                          */

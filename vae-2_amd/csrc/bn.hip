@@ -331,10 +331,13 @@ __global__ __launch_bounds__(256) void partials_reduce_kernel(
 // accumulate dgamma/dbeta (MODE 1: backward).  Used when no cross-rank exchange
 // sits between the reduction and its consumer.
 template <int MODE>
+// mshift (optional): the partials are sums of (x - mshift[c]) (shifted statistics: no
+// cancellation in E[x^2] - E[x]^2 when |mean| >> std); the mean gets the shift back.
 __global__ __launch_bounds__(256) void reduce_then_kernel(
     const float* __restrict__ part, int64_t rows, int64_t C, double* sums, double count,
     const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
-    float momentum, float eps, float* save, float* dgamma, float* dbeta) {
+    float momentum, float eps, float* save, float* dgamma, float* dbeta,
+    const float* mshift = nullptr) {
   __shared__ double red[2][4];
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -361,9 +364,10 @@ __global__ __launch_bounds__(256) void reduce_then_kernel(
     return;
   }
   if (c == 0 && nbt) nbt[0] += 1;
-  const double mean = s0 / count;
-  double var = s1 / count - mean * mean;
+  const double m0 = s0 / count;
+  double var = s1 / count - m0 * m0;
   if (var < 0.0) var = 0.0;
+  const double mean = m0 + (mshift ? (double)mshift[c] : 0.0);
   const double invstd = 1.0 / sqrt(var + (double)eps);
   const float gm = gamma ? gamma[c] : 1.f;
   const float bt = beta ? beta[c] : 0.f;
@@ -382,13 +386,14 @@ __global__ void bn_finalize_kernel(const double* sums, double count,
                                    const float* gamma, const float* beta,
                                    float* rmean, float* rvar, int64_t* nbt,
                                    float momentum, float eps, int64_t C,
-                                   float* save) {
+                                   float* save, const float* mshift = nullptr) {
   int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
-  double mean = sums[c] / count;
-  double var = sums[C + c] / count - mean * mean;
+  const double m0 = sums[c] / count;
+  double var = sums[C + c] / count - m0 * m0;
   if (var < 0.0) var = 0.0;
+  const double mean = m0 + (mshift ? (double)mshift[c] : 0.0);
   double invstd = 1.0 / sqrt(var + (double)eps);
   float g = gamma ? gamma[c] : 1.f;
   float b = beta ? beta[c] : 0.f;
@@ -859,6 +864,37 @@ int vae2_bn_reduce_finalize(const float* partials, int64_t rows, int64_t c,
   VAE2_LAUNCH((reduce_then_kernel<0>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
                      partials, rows, c, sums, count, gamma, beta, running_mean, running_var,
                      num_batches_tracked, momentum, eps, save, (float*)nullptr, (float*)nullptr);
+  return check_launch(fn);
+}
+
+int vae2_bn_reduce_finalize_shifted(const float* partials, int64_t rows, int64_t c,
+                                    double* sums, double count, const float* mean_shift,
+                                    const float* gamma, const float* beta,
+                                    float* running_mean, float* running_var,
+                                    int64_t* num_batches_tracked, float momentum, float eps,
+                                    float* save, void* stream) {
+  const char* fn = "vae2_bn_reduce_finalize_shifted";
+  VAE2_REQUIRE(partials && sums && save && rows > 0 && c > 0 && count > 0, fn, "bad arguments");
+  VAE2_REQUIRE((running_mean == nullptr) == (running_var == nullptr), fn,
+               "running_mean and running_var must both be set or both be null");
+  VAE2_LAUNCH((reduce_then_kernel<0>), dim3((unsigned)c), dim3(256), 0, as_stream(stream),
+              partials, rows, c, sums, count, gamma, beta, running_mean, running_var,
+              num_batches_tracked, momentum, eps, save, (float*)nullptr, (float*)nullptr,
+              mean_shift);
+  return check_launch(fn);
+}
+
+int vae2_bn_finalize_shifted(const double* sums, double count, const float* mean_shift,
+                             const float* gamma, const float* beta, float* running_mean,
+                             float* running_var, int64_t* num_batches_tracked, float momentum,
+                             float eps, int64_t c, float* save, void* stream) {
+  const char* fn = "vae2_bn_finalize_shifted";
+  VAE2_REQUIRE(sums && save && c > 0 && count > 0, fn, "bad arguments");
+  VAE2_REQUIRE((running_mean == nullptr) == (running_var == nullptr), fn,
+               "running_mean and running_var must both be set or both be null");
+  VAE2_LAUNCH(bn_finalize_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0,
+              as_stream(stream), sums, count, gamma, beta, running_mean, running_var,
+              num_batches_tracked, momentum, eps, c, save, mean_shift);
   return check_launch(fn);
 }
 

@@ -338,7 +338,7 @@ struct UpSum {
 template <int NUP>
 __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   extern __shared__ __attribute__((aligned(16))) float usm[];
-  __shared__ float red[2][4][kUsCB];
+  __shared__ double red[2][4][kUsCB];
   f4* tab = reinterpret_cast<f4*>(usm);                  // [NUP][kUsXB] {i0, i1, l0, l1}
   float* vs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [sum_s vcols_s][kUsVS]
   const int lane = threadIdx.x & 63;
@@ -381,13 +381,14 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
              __int_as_float((voff[s] + lx.i1 - vlo[s]) * kUsVS), lx.l0, lx.l1};
     }
   }
-  float bj[4], s1[4], s2[4];
+  float bj[4];
+  double s1[4], s2[4];  // BN partial sums over the band (per-row float sums added in double)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cj = c0 + 16 * j + r;
     bj[j] = (p.bias && cj < p.C) ? p.bias[cj] : 0.f;
-    s1[j] = 0.f;
-    s2[j] = 0.f;
+    s1[j] = 0.0;
+    s2[j] = 0.0;
   }
   const int64_t P = (int64_t)(p.rows / p.nxb / p.nrb) * p.H * p.W;  // n * H * W
   constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
@@ -443,6 +444,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
     __syncthreads();
     // ---- epilogue ----
     const uint32_t ybase = (uint32_t)(cbi * P * 64 + ((int64_t)row * p.W + x0) * 64 + r);
+    float r1[4] = {0.f, 0.f, 0.f, 0.f}, r2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int px = 16 * wave + 4 * g + e;
@@ -457,12 +459,16 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
           const float* vj = vs + 16 * j + r;
           v += t[s][2] * vj[__float_as_int(t[s][0])] + t[s][3] * vj[__float_as_int(t[s][1])];
         }
-        v += bj[j];
         const bool ok = px < xn && c0 + 16 * j + r < p.C;
-        store1(yr, ok ? (ybase + px * 64 + 16 * j) * 4u : kOOB, v);
-        s1[j] += ok ? v : 0.f;
-        s2[j] += ok ? v * v : 0.f;
+        store1(yr, ok ? (ybase + px * 64 + 16 * j) * 4u : kOOB, v + bj[j]);
+        r1[j] += ok ? v : 0.f;  // statistics of y - bias (shifted)
+        r2[j] += ok ? v * v : 0.f;
       }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += (double)r1[j];
+      s2[j] += (double)r2[j];
     }
   }
   if (p.stats) {
@@ -483,10 +489,10 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
     __syncthreads();
     if (wave == 0 && cok) {
       const int rr = (n * p.nrb + oy0 / kUsRows) * p.nxb + xb;
-      p.stats[(int64_t)rr * p.C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] +
-                                       red[0][3][lane];
-      p.stats[((int64_t)p.rows + rr) * p.C + c] = red[1][0][lane] + red[1][1][lane] +
-                                                  red[1][2][lane] + red[1][3][lane];
+      p.stats[(int64_t)rr * p.C + c] =
+          (float)(red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
+      p.stats[((int64_t)p.rows + rr) * p.C + c] =
+          (float)(red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
     }
   }
 }

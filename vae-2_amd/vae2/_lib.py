@@ -79,6 +79,10 @@ _SIGS = {
                                          c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "vae2_head_out_bwd_apply": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp,
                                         c_f64, c_vp, P_ACT, c_vp, c_vp, c_i64, c_vp]),
+    "vae2_bn_reduce_finalize_shifted": (c_int, [c_vp, c_i64, c_i64, c_vp, c_f64, c_vp, c_vp, c_vp,
+                                                c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp]),
+    "vae2_bn_finalize_shifted": (c_int, [c_vp, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_f32, c_f32, c_i64, c_vp, c_vp]),
     "vae2_bn_partial_rows": (c_i64, [P_ACT]),
     "vae2_bn_stats": (c_int, [c_vp, P_ACT, c_vp, c_vp]),
     "vae2_bn_partials_reduce": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_vp]),
@@ -131,7 +135,7 @@ _SIGS = {
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 
 

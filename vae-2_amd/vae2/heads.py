@@ -21,7 +21,8 @@ oracle).  Kernels:
 
   vae2_conv2d_fwd          z_j = W_j y_j              (j >= 1, branch resolution)
   vae2_conv1x1_upsum_fwd   y = W0 y0 + b + sum_j up(z_j), BN partial stats fused
-  vae2_bn_reduce_finalize  BN batch statistics (SyncBN: reduce, all-reduce, finalize)
+  vae2_bn_reduce_finalize_shifted  BN batch statistics of y - b (SyncBN: reduce, all-reduce,
+                           finalize)
   vae2_head_out_fwd        out = W2 ReLU(BN(y)) + b2 (the ReLU output is never stored)
   backward: vae2_head_out_bwd_reduce / _apply (-> dL/dy), vae2_upsample_bilinear_bwd_multi
   (dL/dz_j for all branches, dL/dy read once), vae2_conv2d_bwd_weight_ld (dW_j into
@@ -116,17 +117,18 @@ class _Heads(torch.autograd.Function):
                     if count <= 1:
                         raise ValueError("Expected more than 1 value per channel when training, "
                                          f"got input size {(n, C, H, W)}")
-                    call("vae2_bn_reduce_finalize", ptr(stats), rows, C, ptr(sums), count,
-                         ptr(gamma), ptr(beta), *stat_ptrs, float(bn.momentum), float(bn.eps),
-                         ptr(save), s)
+                    call("vae2_bn_reduce_finalize_shifted", ptr(stats), rows, C, ptr(sums),
+                         count, ptr(b), ptr(gamma), ptr(beta), *stat_ptrs, float(bn.momentum),
+                         float(bn.eps), ptr(save), s)
                     gcount = count
                 else:
                     call("vae2_bn_partials_reduce", ptr(stats), rows, C, ptr(sums), 0, s)
                     sums, gcount = _all_reduce_sums(sums, count, group)
                     if gcount <= 1:
                         raise ValueError("Expected more than 1 value per channel when training")
-                    call("vae2_bn_finalize", ptr(sums), gcount, ptr(gamma), ptr(beta), *stat_ptrs,
-                         float(bn.momentum), float(bn.eps), C, ptr(save), s)
+                    call("vae2_bn_finalize_shifted", ptr(sums), gcount, ptr(b), ptr(gamma),
+                         ptr(beta), *stat_ptrs, float(bn.momentum), float(bn.eps), C, ptr(save),
+                         s)
             else:
                 gcount = count
                 call("vae2_bn_eval_coeffs", ptr(gamma), ptr(beta), ptr(bn.running_mean),
