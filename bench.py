@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--profile-json", default=None,
                     help="write the live per-family / per-kernel / per-shape tables here")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="conv MFMA operand precision (bf16: operands rounded to bf16, fp32 "
+                         "accumulation / storage / BN / optimizer; a separate, looser-"
+                         "tolerance line, BASELINE configs 2 and 5)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto: at N=1)")
     return ap.parse_args()
@@ -190,6 +194,10 @@ def main():
     from vae2.optim import FusedAdam
     config = load_config(args)
     vdist.set_sync_bn(config.MI355X.SYNC_BN)
+    if args.dtype == "bf16":
+        from vae2 import _lib
+        _lib.load().vae2_conv2d_set_mfma_bf16(1)
+        prof.set_mfma_dtype("bf16")
 
     L = config.TRAIN.CLIP_LENGTH
     W, H = config.TRAIN.IMAGE_SIZE
@@ -264,7 +272,8 @@ def main():
             "metric": METRIC,
             "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype,
             "data": "synthetic (Gaussian Cityscapes-shaped clips resident in HBM; random-init "
                     "weights, reference init seed 0)",
             "config": {"workload": f"VAE2 ELBO step (encz + encoder + 2 decoders fwd/bwd + "
@@ -274,7 +283,10 @@ def main():
                        "global_batch": world * B, "frames_per_clip": 3 * L,
                        "image": [H, W], "parallelism": f"dp{world}",
                        "sync_bn": world > 1 and config.MI355X.SYNC_BN,
-                       "launch": "hip_graph" if use_graph else "eager"},
+                       "launch": "hip_graph" if use_graph else "eager",
+                       "mfma_operands": ("bf16 (RNE; fp32 accumulation, fp32 activations in "
+                                         "HBM, fp32 BN / loss / Adam)" if args.dtype == "bf16"
+                                         else "fp32")},
             "last_loss": last_loss,
         }
         if profiler is not None:
@@ -287,11 +299,11 @@ def main():
             tr = pmc_traffic(dom["kernel"])
             roof["traffic"] = round(tr["hbm_bytes_per_launch"]) if tr else None
             roof["traffic_unit"] = "HBM bytes/launch (PMC, profiles/)"
-            roof["step_frac"] = round(conv_gf / ms / prof.FP32_MFMA_PEAK_TF, 4)
+            roof["step_frac"] = round(conv_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["step_gflop"] = round(conv_gf, 1)
             if ref_gf is not None and L == 3:
                 roof["step_frac_ref_flops"] = round(
-                    B * ref_gf / ms / prof.FP32_MFMA_PEAK_TF, 4)
+                    B * ref_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["measured"] = (f"{n} eager steps after the timed region, every C-ABI call "
                                 "timed with HIP events on its stream, isolated from side "
                                 "streams")

@@ -61,6 +61,12 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
  * implicit-GEMM kernel for layers with few row tiles.  Returns the previous setting.
  * Process-wide; set it before building stats buffers.                           */
 int vae2_conv2d_set_algo(int algo);
+/* MFMA operand precision of every conv kernel (forward, data and weight gradient):
+ * 0 = fp32 operands (v_mfma_f32_16x16x4_f32, exact fp32 products; the default),
+ * 1 = bf16 operands (v_mfma_f32_16x16x32_bf16: activations, gradients and weights are
+ * rounded to bf16 (RNE) as they enter the MFMA; accumulation, storage, BatchNorm and the
+ * optimizer stay fp32).  Returns the previous setting.  Process-wide.             */
+int vae2_conv2d_set_mfma_bf16(int on);
 
 /* Conv weights are consumed in a packed layout (zero-padded, K = (tap, 4-channel
  * quad) ordered): mode 0 for vae2_conv2d_fwd  = [round_up(Cout,64)][k*k][round_up(Cin,4)],

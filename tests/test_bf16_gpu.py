@@ -1,0 +1,96 @@
+"""bf16 MFMA operands (vae2_conv2d_set_mfma_bf16, bench.py --dtype bf16) on BASELINE.json
+config 2: Cityscapes-shaped 64x64 clips, 2 context + 4 predicted frames (CLIP_LENGTH 2,
+NUM_CLASSES 2: SURVEY §8 frame mapping), batch 4, HRNet-W18-small-v2.
+
+Every conv rounds its MFMA operands (activations, gradients, weights) to bf16 and
+accumulates in fp32; storage, BatchNorm, the loss and the optimizer stay fp32.  The
+kernels themselves are exact against the fp64 conv of bf16-rounded operands
+(test_kernels_gpu.py::test_conv_bf16_operands).  End to end, against the fp32 CPU oracle
+(oracle/ref_cpu.py), with bf16 tolerances (bf16 is a looser-tolerance
+variant; the same step with fp32 operands keeps the fp32 bounds):
+  forward     loss terms rel 1e-2, x2t_hat rel-L2 5e-2 (fp32 operands: 1e-5 / 1e-4)
+  training    6 Adam steps (lr 3e-3) on one low-amplitude batch (x 0.1): the first
+              loss within 2e-3 of the fp32 run's, every later one within 15 % (the
+              trajectory is chaotic: Adam's first steps move every weight by ~lr;
+              measured deviation <= 7 %).
+Per-tensor gradients are not compared: at the reference's init (conv weights std 1e-3,
+every conv followed by BatchNorm) they are chaotic — fp32 operands already land 6 %
+(median rel-L2) from the fp32 oracle by rounding order alone, and bf16 rounding
+decorrelates them (cosine 0.04 measured) while the loss trajectory is unchanged."""
+import pytest
+import torch
+
+from helpers import build, make_cfg, rel
+from test_model_gpu import DEV, hip_model
+
+pytestmark = pytest.mark.gpu
+KW = dict(arch="w18", hw=(64, 64), L=2, classes=2)
+B = 4
+NAMES = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
+
+
+def _inputs():
+    gen = torch.Generator().manual_seed(11)
+    xs = [torch.randn(B, 6, 64, 64, generator=gen) for _ in range(3)]
+    eps = torch.randn(B, 10, 1, 1, generator=gen)
+    code = torch.randn(B, 10, 1, 1, generator=gen)
+    return xs, eps, code
+
+
+def _set_bf16(on):
+    from vae2 import _lib
+    return _lib.load().vae2_conv2d_set_mfma_bf16(1 if on else 0)
+
+
+def _run(bf16, xs, eps, code, steps=0, lr=1e-3):
+    """HIP forward (+ `steps` Adam steps on the same batch): losses per step, x2t_hat."""
+    from vae2.optim import FusedAdam
+    prev = _set_bf16(bf16)
+    try:
+        torch.manual_seed(0)
+        fm = hip_model(KW)
+        opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=lr)
+        xd = [x.to(DEV) for x in xs]
+        hist, x2 = [], None
+        for i in range(max(steps, 1)):
+            fm.set_noise(eps, code)
+            opt.zero_grad()
+            losses, x1p, x2p, x3p = fm(*xd, 1.0)
+            hist.append([float(v.reshape(-1)[0]) if torch.is_tensor(v) else float(v)
+                         for v in losses[:5]])
+            if i == 0:
+                x2 = x2p.detach().cpu()
+            if steps:
+                losses[0].backward()
+                opt.step()
+        torch.cuda.synchronize()
+    finally:
+        _set_bf16(prev)
+    return hist, x2
+
+
+def test_bf16_config2_forward_against_fp32_oracle():
+    from oracle import ref_cpu
+    xs, eps, code = _inputs()
+    torch.manual_seed(0)
+    ed, ez = build(make_cfg(**KW))
+    with torch.no_grad():
+        terms, preds, _ = ref_cpu.elbo(ez, ed, *xs, eps, code)
+    ref = [float(terms[n]) for n in NAMES]
+    x2_ref = preds[1]
+    for bf16, tl, tx in ((False, 1e-5, 1e-4), (True, 1e-2, 5e-2)):
+        hist, x2p = _run(bf16, xs, eps, code)
+        for n, a, b in zip(NAMES, hist[0], ref):
+            assert abs(a - b) <= tl * abs(b) + 1e-6, (bf16, n, a, b)
+        x2 = x2p.permute(0, 3, 1, 2) if x2p.shape[1] != x2_ref.shape[1] else x2p
+        assert rel(x2, x2_ref) < tx, (bf16, rel(x2, x2_ref))
+
+
+def test_bf16_config2_training_tracks_fp32():
+    xs, eps, code = _inputs()
+    xs = [0.1 * x for x in xs]
+    h32, _ = _run(False, xs, eps, code, steps=6, lr=3e-3)
+    h16, _ = _run(True, xs, eps, code, steps=6, lr=3e-3)
+    assert abs(h16[0][0] - h32[0][0]) <= 2e-3 * h32[0][0]
+    for i, (a, b) in enumerate(zip(h16, h32)):
+        assert abs(a[0] - b[0]) <= 0.15 * abs(b[0]), (i, a[0], b[0])

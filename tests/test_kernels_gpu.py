@@ -118,6 +118,66 @@ def test_direct_conv3x3(shape):
         assert rel(cg.bias.grad, conv.bias.grad) < TOL
 
 
+BF16_SHAPES = [
+    # N, H, W, Cin, Cout, k, stride, bias, algo: every conv kernel with bf16 operands
+    (2, 16, 32, 18, 18, 3, 1, False, 2),    # direct 3x3 (dconv3 fwd / dgrad, wgrad3)
+    (2, 13, 40, 36, 36, 3, 1, True, 2),     # partial tiles, 2 slabs
+    (1, 8, 32, 154, 144, 3, 1, False, 2),   # 5 slabs, N split
+    (2, 17, 13, 9, 64, 3, 1, False, 1),     # gather kernel (igemm), channel-pad quad
+    (2, 16, 16, 36, 72, 3, 2, False, 0),    # stride 2 (igemm, parity-class dgrad, wgrad)
+    (2, 8, 8, 270, 270, 1, 1, True, 0),     # 1x1
+    (1, 128, 512, 72, 270, 1, 1, True, 0),  # wide-N 1x1 tiles
+    (2, 12, 20, 256, 18, 3, 1, False, 0),   # K split
+]
+
+
+@pytest.mark.parametrize("shape", BF16_SHAPES)
+def test_conv_bf16_operands(shape):
+    """vae2_conv2d_set_mfma_bf16(1): every conv kernel rounds its MFMA operands to bf16
+    (RNE) and accumulates in fp32, so forward, data gradient and weight gradient equal
+    the fp64 conv of the bf16-rounded x, w and dy up to fp32 summation order."""
+    from vae2 import _lib, ops
+    torch.manual_seed(4)
+    n, h, w, cin, cout, k, s, bias, algo = shape
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=bias)
+    x = torch.randn(n, cin, h, w)
+    ho, wo = (h + 2 * (k // 2) - k) // s + 1, (w + 2 * (k // 2) - k) // s + 1
+    gy = torch.randn(n, cout, ho, wo)
+
+    def bf(t):
+        return t.bfloat16().double()
+    x64 = bf(x).requires_grad_(True)
+    w64 = bf(conv.weight.detach()).requires_grad_(True)
+    b64 = conv.bias.detach().double() if bias else None
+    y64 = F.conv2d(x64, w64, b64, s, k // 2)
+    y64.backward(bf(gy))
+    cg = nn.Conv2d(cin, cout, k, s, k // 2, bias=bias).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    lib = _lib.load()
+    prev_algo = lib.vae2_conv2d_set_algo(algo)
+    prev_bf = lib.vae2_conv2d_set_mfma_bf16(1)
+    try:
+        xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+        with torch.no_grad():
+            xg.copy_(nhwc(x).to(DEV))
+        xg.requires_grad_(True)
+        yg = ops.conv(xg, cg)
+        yg.backward(nhwc(gy).to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        lib.vae2_conv2d_set_mfma_bf16(prev_bf)
+        lib.vae2_conv2d_set_algo(prev_algo)
+    tol = 3e-5
+    assert rel(nchw(yg).double(), y64) < tol
+    assert rel(nchw(xg.grad).double(), x64.grad) < tol
+    assert rel(cg.weight.grad.double(), w64.grad) < tol
+    if bias:
+        assert rel(cg.bias.grad.double(), gy.double().sum((0, 2, 3))) < tol
+    # and the bf16 rounding itself is visible against the fp32 conv (the path ran)
+    y32 = F.conv2d(x, conv.weight.detach(), conv.bias.detach() if bias else None, s, k // 2)
+    assert rel(nchw(yg).cpu(), y32) > 1e-4
+
+
 def ctypes_name(x, yshape):
     from vae2 import ops, prof
     _, xa = ops.act_of(x)

@@ -54,6 +54,16 @@ __device__ __forceinline__ float load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// bf16 MFMA operands (v_mfma_f32_16x16x32_bf16): lane (g, r) holds k = 8g .. 8g+7; the
+// conv kernels pair two of their fp32 K chunks (4 consecutive k per lane each) into one
+// fragment, A and B from the same chunks, so any k order within a chunk pair is shared.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x8 pack_bf16(f4 a, f4 b) {
+  typedef float f8 __attribute__((ext_vector_type(8)));
+  const f8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_convertvector(v, bf16x8);  // v_cvt_pk_bf16_f32 (RNE, NaN kept)
+}
+
 __device__ __forceinline__ void store1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
 }

@@ -116,7 +116,7 @@ struct IGemm {
 // KS = 4: in-workgroup K split for layers with too few row tiles to fill the chip: the 4
 // waves share one (16*TM)-row tile, wave w takes K chunks w, w+4, ..., and the partial
 // tiles are summed in LDS in a fixed order (deterministic) before wave 0's epilogue.
-template <int TM, int TN, bool VEC, int ROLE, int KS = 1>
+template <int TM, int TN, bool VEC, int ROLE, int KS = 1, bool BF = false>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   IGemm p = pin;
   if (gridDim.z > 1) {
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   };
 
   // Chunk pairs; the (possibly) extra odd chunk loads zeros (tt >= ntaps).
-  if (mw < M) {
+  if (mw < M && !BF) {
     int mk0 = 0, mk1 = 0;
     load(fa0, fb0, mk0);
     for (int ch = 0; ch < nchunks; ch += 2) {
@@ -235,6 +235,35 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       mma(fa0, fb0, mk0);
       load(fa0, fb0, mk0);
       mma(fa1, fb1, mk1);
+    }
+  } else if (mw < M) {  // bf16 operands: one 16x16x32 MFMA per chunk pair
+    int mk0 = 0, mk1 = 0;
+    load(fa0, fb0, mk0);
+    load(fa1, fb1, mk1);
+    for (int ch = 0; ch < nchunks; ch += 2) {
+      if (VEC && cpad) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          fa0[i][1] = (mk0 & 2) ? fa0[i][1] : 0.f;
+          fa0[i][2] = (mk0 & 4) ? fa0[i][2] : 0.f;
+          fa0[i][3] = (mk0 & 8) ? fa0[i][3] : 0.f;
+          fa1[i][1] = (mk1 & 2) ? fa1[i][1] : 0.f;
+          fa1[i][2] = (mk1 & 4) ? fa1[i][2] : 0.f;
+          fa1[i][3] = (mk1 & 8) ? fa1[i][3] : 0.f;
+        }
+      }
+      bf16x8 A[TM], B[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) A[i] = pack_bf16(fa0[i], fa1[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) B[j] = pack_bf16(fb0[j], fb1[j]);
+      load(fa0, fb0, mk0);
+      load(fa1, fb1, mk1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
     }
   }
 
@@ -357,7 +386,7 @@ struct DConv {
 constexpr int kDcBW = 32;     // tile columns
 constexpr int kDcMaxCs4 = 8;  // quads per slab
 
-template <int TM, int TN, bool FLIP>
+template <int TM, int TN, bool FLIP, bool BF = false>
 __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
   constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
@@ -447,12 +476,31 @@ __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
       q += 4;
       while (q >= qs) { q -= qs; ++t; }
     };
-    load(fa0, fb0);
-    for (int ch = 0; ch < nch; ch += 2) {
-      load(fa1, fb1);
-      mma(fa0, fb0);
+    if (!BF) {
       load(fa0, fb0);
-      mma(fa1, fb1);
+      for (int ch = 0; ch < nch; ch += 2) {
+        load(fa1, fb1);
+        mma(fa0, fb0);
+        load(fa0, fb0);
+        mma(fa1, fb1);
+      }
+    } else {  // bf16 operands: one 16x16x32 MFMA per chunk pair
+      load(fa0, fb0);
+      load(fa1, fb1);
+      for (int ch = 0; ch < nch; ch += 2) {
+        bf16x8 A[TM], B[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) A[i] = pack_bf16(fa0[i], fa1[i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) B[j] = pack_bf16(fb0[j], fb1[j]);
+        load(fa0, fb0);
+        load(fa1, fb1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
 
@@ -549,6 +597,7 @@ static Tile pick_tile(int64_t M, int N, bool wide = false) {
 }
 
 static int g_ksplit = 1;  // vae2_conv2d_set_algo bit 8 disables the K split (A/B tests)
+static int g_bf16 = 0;    // vae2_conv2d_set_mfma_bf16: bf16 MFMA operands (fp32 accumulate)
 
 static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   const bool wide = wide_ok(M, N, taps);
@@ -563,7 +612,10 @@ template <int TM, bool VEC, int ROLE, int KS = 1>
 static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((igemm_kernel<TM, T, VEC, ROLE, KS>), grid, dim3(256), 0, s, p); break;
+  case T:                                                                         \
+    if (g_bf16) VAE2_LAUNCH((igemm_kernel<TM, T, VEC, ROLE, KS, true>), grid, dim3(256), 0, s, p); \
+    else VAE2_LAUNCH((igemm_kernel<TM, T, VEC, ROLE, KS>), grid, dim3(256), 0, s, p);   \
+    break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
@@ -573,7 +625,10 @@ template <bool VEC, int ROLE>
 static void launch_wide(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((igemm_kernel<2, T, VEC, ROLE>), grid, dim3(256), 0, s, p); break;
+  case T:                                                                         \
+    if (g_bf16) VAE2_LAUNCH((igemm_kernel<2, T, VEC, ROLE, 1, true>), grid, dim3(256), 0, s, p); \
+    else VAE2_LAUNCH((igemm_kernel<2, T, VEC, ROLE>), grid, dim3(256), 0, s, p);       \
+    break;
     CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
 #undef CASE
   }
@@ -652,7 +707,7 @@ struct WGrad {
   FastDiv ohw_div, ow_div, cin4_div;
 };
 
-template <int TM, int TN>
+template <int TM, int TN, bool BF = false>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
   extern __shared__ __attribute__((aligned(16))) float wred[];  // [3][TM*TN*4][64]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -729,12 +784,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
   {
     f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
     int pc = pbeg + 16 * wave;
-    if (pc < pend) load(pc, fa0, fb0);
-    for (; pc < pend; pc += 128) {
+    if (!BF) {
+      if (pc < pend) load(pc, fa0, fb0);
+      for (; pc < pend; pc += 128) {
+        load(pc + 64, fa1, fb1);
+        mma(fa0, fb0);
+        load(pc + 128, fa0, fb0);
+        mma(fa1, fb1);
+      }
+    } else if (pc < pend) {  // bf16 operands: one 16x16x32 MFMA per chunk pair
+      load(pc, fa0, fb0);
       load(pc + 64, fa1, fb1);
-      mma(fa0, fb0);
-      load(pc + 128, fa0, fb0);
-      mma(fa1, fb1);
+      for (; pc < pend; pc += 128) {
+        bf16x8 A[TM], B[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) A[i] = pack_bf16(fa0[i], fa1[i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) B[j] = pack_bf16(fb0[j], fb1[j]);
+        load(pc + 128, fa0, fb0);
+        load(pc + 192, fa1, fb1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
 
@@ -794,7 +868,7 @@ struct WGrad3 {
   float* part;  // [splits][cout][9*cin4]
 };
 
-template <int TM, int TN, int BH, bool PF, int KS>
+template <int TM, int TN, int BH, bool PF, int KS, bool BF = false>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   constexpr int HALO = KS / 2, TAPS = KS * KS;
   constexpr int LH = BH + KS - 1, LW = 32 + KS - 1, NPX = BH * 32, LPX = LH * LW;
@@ -940,11 +1014,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     }
     __syncthreads();
     if (PF && tile + 1 < te) fetch(tile + 1);
-#pragma unroll 2
-    for (int ch = 0; ch < NPX / 16; ++ch) {
+    auto frag = [&](int ch, f4* fa, f4* fb) {
       const int px0 = ch * 16 + 4 * g;
       const int poff = (px0 >> 5) * LW + (px0 & 31);
-      f4 fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         fa[i] = *reinterpret_cast<const f4*>(&dyt[(i * 16 + r) * DYS + px0]);
@@ -954,13 +1026,33 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
         if (KS == 1) fb[j] = *reinterpret_cast<const f4*>(b);  // 16-byte aligned: no tap shift
         else fb[j] = f4{b[0], b[1], b[2], b[3]};
       }
+    };
+    if (!BF) {
+#pragma unroll 2
+      for (int ch = 0; ch < NPX / 16; ++ch) {
+        f4 fa[TM], fb[TN];
+        frag(ch, fa, fb);
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2)
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+      }
+    } else {  // bf16 operands: one 16x16x32 MFMA per pair of 16-pixel chunks
+#pragma unroll 2
+      for (int ch = 0; ch < NPX / 16; ch += 2) {
+        f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+        frag(ch, fa0, fb0);
+        frag(ch + 1, fa1, fb1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                pack_bf16(fa0[i], fa1[i]), pack_bf16(fb0[j], fb1[j]), acc[i][j], 0, 0, 0);
+      }
     }
   }
 
@@ -1049,10 +1141,22 @@ template <int TM>
 static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)3 * TM * 4 * 4 * 64 * sizeof(float) / 4 * tn;  // 3 waves x NV x 64
   switch (tn) {
-    case 1: VAE2_LAUNCH((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p); break;
-    case 2: VAE2_LAUNCH((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p); break;
-    case 3: VAE2_LAUNCH((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p); break;
-    default: VAE2_LAUNCH((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p); break;
+    case 1:
+      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 1, true>), grid, dim3(256), lds, s, p);
+      else VAE2_LAUNCH((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p);
+      break;
+    case 2:
+      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 2, true>), grid, dim3(256), lds, s, p);
+      else VAE2_LAUNCH((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p);
+      break;
+    case 3:
+      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 3, true>), grid, dim3(256), lds, s, p);
+      else VAE2_LAUNCH((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p);
+      break;
+    default:
+      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 4, true>), grid, dim3(256), lds, s, p);
+      else VAE2_LAUNCH((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p);
+      break;
   }
 }
 
@@ -1127,7 +1231,10 @@ template <int TM, bool FLIP>
 static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
   switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p); break;
+  case T:                                                                         \
+    if (g_bf16) VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, true>), grid, dim3(256), shm, s, p); \
+    else VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p);        \
+    break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
   }
@@ -1223,12 +1330,16 @@ template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
                              hipStream_t s) {
   if (ks == 1) {  // 1x1: at most 64 channels = 4 column tiles per slab, one per wave
-    VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
+    if (g_bf16) VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1, true>), grid, dim3(256), shm, s, p);
+    else VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
     return;
   }
   switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p); break;
+  case T:                                                                         \
+    if (g_bf16) VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, true>), grid, dim3(256), shm, s, p); \
+    else VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p);   \
+    break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
 #undef CASE
   }
@@ -1283,6 +1394,12 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
   VAE2_LAUNCH(pack_weights_batched_kernel, dim3(32, (unsigned)njobs), dim3(256), 0,
                      as_stream(stream), jobs);
   return check_launch(fn);
+}
+
+int vae2_conv2d_set_mfma_bf16(int on) {
+  const int prev = g_bf16;
+  g_bf16 = on ? 1 : 0;
+  return prev;
 }
 
 int vae2_conv2d_set_algo(int algo) {

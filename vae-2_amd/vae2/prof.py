@@ -26,8 +26,8 @@ _ACTIVE = None
 
 # (family, regex on a kernel name), first match wins (also used by tools/trace_steps.py)
 FAMILIES = (
-    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false>|igemm_kernel<\d+, \d+, \w+, 0"),
-    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true>|igemm_kernel<\d+, \d+, \w+, [12]"),
+    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false|igemm_kernel<\d+, \d+, \w+, 0"),
+    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true|igemm_kernel<\d+, \d+, \w+, [12]"),
     ("conv_wgrad", r"wgrad"),
     ("batchnorm", r"bn_|reduce_then|chan_partials|partials_reduce"),
     ("heads", r"upsum|head_|up_adj"),
@@ -39,8 +39,16 @@ FAMILIES = (
     ("copies", r"rocclr_copy|rocclr_fill"),
 )
 
-FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E
+FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense (no sparsity)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E
+MFMA_PEAK_TF = FP32_MFMA_PEAK_TF  # the conv MFMA operand dtype in use (set_mfma_dtype)
+
+
+def set_mfma_dtype(dtype):
+    """Price conv FLOPs against the peak of the MFMA operand dtype ("fp32" / "bf16")."""
+    global MFMA_PEAK_TF
+    MFMA_PEAK_TF = BF16_MFMA_PEAK_TF if dtype == "bf16" else FP32_MFMA_PEAK_TF
 
 
 def family(kernel):
@@ -146,7 +154,7 @@ class StepProfiler:
                 if fl:
                     r["gflop_per_step"] = round(fl / steps / 1e9, 3)
                     r["tflops"] = round(fl / (ms * 1e-3) / 1e12, 2)
-                    r["frac_fp32_peak"] = round(fl / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4)
+                    r["frac_mfma_peak"] = round(fl / (ms * 1e-3) / 1e12 / MFMA_PEAK_TF, 4)
                 if by:
                     r["gb_per_step"] = round(by / steps / 1e9, 3)
                     r["gbs"] = round(by / (ms * 1e-3) / 1e9, 1)
@@ -179,7 +187,7 @@ class StepProfiler:
                "algorithmic_bytes_per_launch": by / n}
         if fl > 0:
             out.update(bound="mfma", achieved=round(fl / n / avg_s / 1e12, 3),
-                       peak=FP32_MFMA_PEAK_TF, unit="TFLOP/s")
+                       peak=MFMA_PEAK_TF, unit="TFLOP/s")
         else:
             out.update(bound="hbm", achieved=round(by / n / avg_s / 1e9, 1),
                        peak=HBM_PEAK_GBS, unit="GB/s")
