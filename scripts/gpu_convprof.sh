@@ -7,13 +7,13 @@ ONLY=${2:-3}
 RX=${3:-"dconv3|igemm|wgrad"}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python vae-2_amd/tools/conv_bench.py --only $ONLY --iters 10 \
+timeout -k 10 300 python vae-2_amd/tools/conv_bench.py --only $ONLY --iters 10 $EXTRA \
   > gpurun_out/${TAG}_bench.log 2>&1 || { tail gpurun_out/${TAG}_bench.log; exit 1; }
 cat gpurun_out/${TAG}_bench.log
 pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$RX" -f csv \
-    -d gpurun_out/${TAG}_pmc_$name -o run -- python vae-2_amd/tools/conv_bench.py --only $ONLY --iters 2 \
+    -d gpurun_out/${TAG}_pmc_$name -o run -- python vae-2_amd/tools/conv_bench.py --only $ONLY --iters 2 $EXTRA \
     > gpurun_out/${TAG}_pmc_$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac

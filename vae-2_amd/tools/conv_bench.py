@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--algo", type=int, nargs="*", default=[0],
                     help="vae2_conv2d_set_algo values to compare (0 auto, 1 gather, 2 direct)")
     ap.add_argument("--all", action="store_true", help="every ELBO conv shape (ALL_SHAPES)")
+    ap.add_argument("--bf16", action="store_true", help="bf16 MFMA operands")
     a = ap.parse_args()
     if a.all:
         SHAPES[:] = ALL_SHAPES
@@ -79,6 +80,7 @@ def main():
     torch.cuda.synchronize()
     for algo in a.algo:
         lib.vae2_conv2d_set_algo(algo)
+        lib.vae2_conv2d_set_mfma_bf16(1 if a.bf16 else 0)
         print(f"== algo {algo}")
         run(a, lib)
 
