@@ -67,6 +67,14 @@ int vae2_conv2d_set_algo(int algo);
  * rounded to bf16 (RNE) as they enter the MFMA; accumulation, storage, BatchNorm and the
  * optimizer stay fp32).  Returns the previous setting.  Process-wide.             */
 int vae2_conv2d_set_mfma_bf16(int on);
+/* Deferred weight-gradient reductions (per calling thread): while on, every
+ * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
+ * reduction; vae2_wgrad_flush launches the queued reductions together (up to 8 per
+ * launch, in queue order, each on the stream its weight gradient was issued on).  The
+ * caller keeps each call's workspace alive until the flush is enqueued and does not
+ * queue two reductions into the same dW elements.  Returns the previous setting.   */
+int vae2_wgrad_defer(int on);
+int vae2_wgrad_flush(void* stream);
 
 /* Conv weights are consumed in a packed layout (zero-padded, K = (tap, 4-channel
  * quad) ordered): mode 0 for vae2_conv2d_fwd  = [round_up(Cout,64)][k*k][round_up(Cin,4)],

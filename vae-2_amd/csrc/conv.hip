@@ -21,6 +21,8 @@
 //
 // Replaces nn.Conv2d forward/backward for every conv of enc_hrnet.py (call sites
 // in include/vae2_hip.h).
+#include <vector>
+
 #include "common.h"
 
 namespace vae2 {
@@ -1112,6 +1114,60 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
+// Deferred reductions (vae2_wgrad_defer / vae2_wgrad_flush): the weight gradients of
+// one BatchNorm depth level (the lock-stepped branch convs, a head's branch blocks) share
+// one reduce launch; blocks are partitioned between the jobs by prefix.
+struct WRJob {
+  const float* part;
+  float* dw;
+  int64_t ld;
+  int splits, cout, cin, cin4, k, accumulate, blk0;
+};
+constexpr int kWrMaxJobs = 8;
+struct WRMulti {
+  WRJob j[kWrMaxJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_multi_kernel(WRMulti m) {
+  int i = 0;
+  while (i + 1 < m.n && (int)blockIdx.x >= m.j[i + 1].blk0) ++i;
+  const WRJob& J = m.j[i];
+  __shared__ float red[8][32];
+  const int kk = J.k * J.k;
+  const int ncol4 = kk * J.cin4;
+  const int total = J.cout * ncol4;
+  const int cl = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const int idx = ((int)blockIdx.x - J.blk0) * 32 + cl;
+  float s = 0.f;
+  if (idx < total) {
+    const float* src = J.part + idx;
+    const int64_t stride = (int64_t)total;
+#pragma unroll 8
+    for (int sp = sg; sp < J.splits; sp += 8) s += src[sp * stride];
+  }
+  red[sg][cl] = s;
+  __syncthreads();
+  if (sg != 0 || idx >= total) return;
+  s = red[0][cl];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) s += red[q][cl];
+  const int co = idx / ncol4;
+  const int col = idx - co * ncol4;
+  const int t = col / J.cin4;
+  const int ci = col - t * J.cin4;
+  if (ci >= J.cin) return;
+  const int64_t o = (int64_t)co * J.ld + ci * kk + t;
+  J.dw[o] = J.accumulate ? J.dw[o] + s : s;
+}
+
+struct WRQueued {
+  WRJob job;
+  hipStream_t stream;
+};
+static thread_local bool g_wr_defer = false;
+static thread_local std::vector<WRQueued> g_wr_queue;
+
 struct WTile {
   int tm, tn, gx, gy, splits, px_split;
 };
@@ -1402,6 +1458,37 @@ int vae2_conv2d_set_mfma_bf16(int on) {
   return prev;
 }
 
+int vae2_wgrad_defer(int on) {
+  const int prev = g_wr_defer ? 1 : 0;
+  g_wr_defer = on != 0;
+  return prev;
+}
+
+int vae2_wgrad_flush(void* stream) {
+  const char* fn = "vae2_wgrad_flush";
+  hipStream_t want = as_stream(stream);
+  std::vector<WRQueued> q;
+  q.swap(g_wr_queue);
+  size_t i = 0;
+  while (i < q.size()) {  // consecutive jobs of one stream, kWrMaxJobs per launch
+    WRMulti m{};
+    hipStream_t st = q[i].stream;
+    int blocks = 0;
+    while (i < q.size() && m.n < kWrMaxJobs && q[i].stream == st) {
+      WRJob j = q[i].job;
+      j.blk0 = blocks;
+      blocks += (int)ceil_div((int64_t)j.cout * j.k * j.k * j.cin4, 32);
+      m.j[m.n++] = j;
+      ++i;
+    }
+    VAE2_LAUNCH(wgrad_reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    const int rc = check_launch(fn);
+    if (rc) return rc;
+  }
+  (void)want;
+  return 0;
+}
+
 int vae2_conv2d_set_algo(int algo) {
   const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8);
   const int a = algo & 7;
@@ -1605,11 +1692,17 @@ int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* d
   }
 reduce:
   int64_t slab = dyd->c * (int64_t)ncol4;
-  VAE2_LAUNCH(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,
-                     (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw, dw_ld,
-                     accumulate);
-  int rc = check_launch(fn);
-  if (rc) return rc;
+  int rc = 0;
+  if (g_wr_defer) {
+    WRJob j{ws, dw, dw_ld, splits, (int)dyd->c, (int)xd->c, cin4, k, accumulate, 0};
+    g_wr_queue.push_back(WRQueued{j, s});
+  } else {
+    VAE2_LAUNCH(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,
+                (const float*)ws, splits, (int)dyd->c, (int)xd->c, cin4, k, dw, dw_ld,
+                accumulate);
+    rc = check_launch(fn);
+    if (rc) return rc;
+  }
   if (dbias) {
     // bias partial rows live after the largest partial-slab area the workspace holds
     const int64_t part_max = vae2_conv2d_bwd_weight_ws_size(xd, dyd, k) - 4 -

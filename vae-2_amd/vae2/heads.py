@@ -34,8 +34,8 @@ import torch
 
 from . import _lib
 from ._lib import Act, call
-from .ops import (_all_reduce_sums, _bn_group, _empty, _grad_sink, act_of, as_act, new_act,
-                  packed_weight_cols, ptr, stream_ptr)
+from .ops import (_WS_HOLD, _all_reduce_sums, _bn_group, _empty, _grad_sink, act_of, as_act,
+                  new_act, packed_weight_cols, ptr, stream_ptr, wgrad_batch)
 
 _PER_HEAD = 6  # conv weight, conv bias, BN weight, BN bias, out weight, out bias
 
@@ -203,25 +203,28 @@ class _Heads(torch.autograd.Function):
                 call("vae2_upsample_bilinear_bwd_multi", dyp, ctypes.byref(dya), nb - 1, gptrs,
                      gacts, ptr(uws), usz, s)
             c0 = 0
-            for j in range(nb):
-                xj = ys[j]
-                g, gp, ga = gs[j]
-                xjp, xja = act_of(xj)
-                if wsink is not None:
-                    wsz2 = lib.vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xja), ctypes.byref(ga), 1)
-                    ws2 = _empty((max(wsz2, 1),), xj)
-                    call("vae2_conv2d_bwd_weight_ld", xjp, ctypes.byref(xja), gp, ctypes.byref(ga),
-                         ctypes.c_void_p(wsink.data_ptr() + 4 * c0), C, None, 1, 1, 0, 1,
-                         ptr(ws2), wsz2, s)
-                if ctx.needs_input_grad[2 + j]:
-                    first = dxs[j] is None
-                    if first:
-                        dxs[j] = new_act(tuple(xj.shape), xj)
-                    dxp, dxa = act_of(dxs[j])
-                    call("vae2_conv2d_bwd_data", gp, ctypes.byref(ga),
-                         ptr(packed_weight_cols(w, split, j, 1)), dxp, ctypes.byref(dxa), 1, 1, 0,
-                         0.0 if first else 1.0, s)
-                c0 += split[j]
+            with wgrad_batch():  # the branch blocks' dW reductions in one launch
+                for j in range(nb):
+                    xj = ys[j]
+                    g, gp, ga = gs[j]
+                    xjp, xja = act_of(xj)
+                    if wsink is not None:
+                        wsz2 = lib.vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xja),
+                                                                  ctypes.byref(ga), 1)
+                        ws2 = _empty((max(wsz2, 1),), xj)
+                        call("vae2_conv2d_bwd_weight_ld", xjp, ctypes.byref(xja), gp,
+                             ctypes.byref(ga), ctypes.c_void_p(wsink.data_ptr() + 4 * c0), C,
+                             None, 1, 1, 0, 1, ptr(ws2), wsz2, s)
+                        _WS_HOLD.append(ws2)
+                    if ctx.needs_input_grad[2 + j]:
+                        first = dxs[j] is None
+                        if first:
+                            dxs[j] = new_act(tuple(xj.shape), xj)
+                        dxp, dxa = act_of(dxs[j])
+                        call("vae2_conv2d_bwd_data", gp, ctypes.byref(ga),
+                             ptr(packed_weight_cols(w, split, j, 1)), dxp, ctypes.byref(dxa), 1,
+                             1, 0, 0.0 if first else 1.0, s)
+                    c0 += split[j]
             pgrads += [wret, bret, gret, btret, w2ret, b2ret]
         return (None, None, *dxs, *pgrads)
 

@@ -294,6 +294,31 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     return y
 
 
+_WGRAD_BATCH = [0]  # open wgrad_batch contexts
+_WS_HOLD = []       # workspaces of queued weight-gradient reductions
+
+
+class wgrad_batch:
+    """Context: the weight-gradient slab reductions of the convs in it share launches
+    (vae2_wgrad_defer / vae2_wgrad_flush, up to 8 per launch); their workspaces are held
+    until the flush is enqueued (stream order then frees them safely)."""
+
+    def __enter__(self):
+        _lib.load().vae2_wgrad_defer(1)
+        _WGRAD_BATCH[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _WGRAD_BATCH[0] -= 1
+        if _WGRAD_BATCH[0] == 0:
+            try:
+                call("vae2_wgrad_flush", stream_ptr())
+            finally:
+                _lib.load().vae2_wgrad_defer(0)
+                _WS_HOLD.clear()
+        return False
+
+
 def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
     """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b)."""
     s = stream_ptr()
@@ -311,6 +336,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
             _conv_work("wgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya), ptr(wsink),
              ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
+        if _WGRAD_BATCH[0]:
+            _WS_HOLD.append(ws)
     dx = None
     if need_dx:
         link = spec.x_link
@@ -616,21 +643,22 @@ class _ConvBNMulti(torch.autograd.Function):
                              for r, h_, d in zip(rs, ctx.has_res, dress)))
         call("vae2_bn_multi_bwd_apply", n, lay, s)
         grads = [None]
-        for i in range(n):
-            spec = specs[i]
-            x = xs[i]
-            weight, bias = ctx.params[i][0], ctx.params[i][1]
-            dres, gret, bret = dress[i]
-            link = spec.res_link
-            if dres is not None and link is not None:
-                if link.buf is None:
-                    link.buf = dres
-                else:
-                    link.buf.add_(dres)
-                dres = link.finish()
-            dx, wret, bret_conv = _conv_bwd(x, weight, bias, drs[i], spec, need[1 + 6 * i],
-                                            need[1 + 6 * i + 1], need[1 + 6 * i + 2])
-            grads += [dx, wret, bret_conv, gret, bret, dres]
+        with wgrad_batch():  # the level's weight-gradient reductions in one launch
+            for i in range(n):
+                spec = specs[i]
+                x = xs[i]
+                weight, bias = ctx.params[i][0], ctx.params[i][1]
+                dres, gret, bret = dress[i]
+                link = spec.res_link
+                if dres is not None and link is not None:
+                    if link.buf is None:
+                        link.buf = dres
+                    else:
+                        link.buf.add_(dres)
+                    dres = link.finish()
+                dx, wret, bret_conv = _conv_bwd(x, weight, bias, drs[i], spec, need[1 + 6 * i],
+                                                need[1 + 6 * i + 1], need[1 + 6 * i + 2])
+                grads += [dx, wret, bret_conv, gret, bret, dres]
         return tuple(grads)
 
 
