@@ -354,6 +354,13 @@ int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,
                   const vae2_act* yd, float* g, const vae2_act* gd,
                   void* stream);
 
+/* g = dy * (y > 0) and g2 = g + beta2 * g2 in one pass: the ReLU gradient of an HRNet
+ * fuse output handed both to its own consumers and, accumulated, to the shared
+ * gradient buffer of a branch input with several consumers (vae2/ops.py GradLink).  */
+int vae2_relu_bwd_dual(const float* dy, const vae2_act* dyd, const float* y,
+                       const vae2_act* yd, float* g, const vae2_act* gd, float* g2,
+                       const vae2_act* g2d, float beta2, void* stream);
+
 /* y = x (strided NHWC copy, e.g. into a channel slice for torch.cat).         */
 int vae2_copy_act(const float* x, const vae2_act* xd, float* y,
                   const vae2_act* yd, float beta, void* stream);

@@ -274,6 +274,25 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__
   }
 }
 
+// g = dy * [y > 0] and g2 = g + beta2 * g2 (the same gradient handed to a second,
+// accumulating consumer: ops.GradLink of a fuse input, no extra add kernel).
+__global__ __launch_bounds__(256) void relu_bwd_dual_kernel(
+    const float* __restrict__ dy, Act dyd, const float* __restrict__ y, Act yd,
+    float* __restrict__ g, Act gd, float* __restrict__ g2, Act g2d, float beta2, FastDiv cdiv) {
+  const uint32_t C = (uint32_t)yd.c;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    uint32_t p = cdiv.div(i);
+    uint32_t c = i - p * C;
+    float v = dy[(int64_t)p * dyd.ps + c];
+    v = (y[(int64_t)p * yd.ps + c] > 0.f) ? v : 0.f;
+    g[(int64_t)p * gd.ps + c] = v;
+    float* d2 = g2 + (int64_t)p * g2d.ps + c;
+    *d2 = beta2 != 0.f ? v + beta2 * *d2 : v;
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_act_kernel(const float* __restrict__ x, Act xd,
                                                        float* __restrict__ y, Act yd, float beta,
                                                        FastDiv cdiv) {
@@ -523,6 +542,21 @@ int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,
   int64_t total = act_elems(yd);
   VAE2_LAUNCH(relu_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
                      dy, to_act(dyd), y, to_act(yd), g, to_act(gd), FastDiv((uint32_t)yd->c));
+  return check_launch(fn);
+}
+
+int vae2_relu_bwd_dual(const float* dy, const vae2_act* dyd, const float* y,
+                       const vae2_act* yd, float* g, const vae2_act* gd, float* g2,
+                       const vae2_act* g2d, float beta2, void* stream) {
+  const char* fn = "vae2_relu_bwd_dual";
+  VAE2_REQUIRE(dy && y && g && g2 && act_ok(dyd) && act_ok(yd) && act_ok(gd) && act_ok(g2d),
+               fn, "bad arguments");
+  VAE2_REQUIRE(same_hw(dyd, yd) && same_hw(yd, gd) && same_hw(yd, g2d) && dyd->c == yd->c &&
+                   gd->c == yd->c && g2d->c == yd->c, fn, "shape mismatch");
+  int64_t total = act_elems(yd);
+  VAE2_LAUNCH(relu_bwd_dual_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
+              dy, to_act(dyd), y, to_act(yd), g, to_act(gd), g2, to_act(g2d), beta2,
+              FastDiv((uint32_t)yd->c));
   return check_launch(fn);
 }
 

@@ -102,13 +102,13 @@ def _run_convbn_seq(seq, x, x_link=None):
     return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2, x_link=x_link)
 
 
-def _run_convbn_seqs(seqs, xs):
+def _run_convbn_seqs(seqs, xs, x_links=None):
     """Independent Sequential(Conv2d, BatchNorm2d[, ReLU]) units of one depth level,
     their BatchNorm steps in shared launches (ops.conv_bn_multi)."""
     if not seqs:
         return []
     return ops.conv_bn_multi(xs, [q[0] for q in seqs], [q[1] for q in seqs],
-                             [len(q) > 2 for q in seqs])
+                             [len(q) > 2 for q in seqs], x_links=x_links)
 
 
 def run_blocks_lockstep(blocks, xs):
@@ -218,25 +218,32 @@ class HighResolutionModule(nn.Module):
         if nb == 1:
             return xs
         # fuse (enc_hrnet.py:233-249): every j > i 1x1 conv + BN in one batch (upsampled
-        # in the fuse kernel), the j < i stride-2 chains batched by chain position
+        # in the fuse kernel), the j < i stride-2 chains batched by chain position.
+        # Branch output j feeds one unit per fuse row (its identity term in row j, an
+        # up or down path in the others): their gradients meet in one buffer
+        # (ops.GradLink) instead of autograd add kernels.
         rows = list(enumerate(self.fuse_layers))
+        links = [ops.GradLink(len(rows)) if len(rows) > 1 else None for _ in range(nb)]
         terms = {}
         ups = [(i, j) for i, _ in rows for j in range(nb) if j > i]
         for (i, j), t in zip(ups, _run_convbn_seqs([self.fuse_layers[i][j] for i, j in ups],
-                                                  [xs[j] for _, j in ups])):
+                                                  [xs[j] for _, j in ups],
+                                                  [links[j] for _, j in ups])):
             terms[(i, j)] = t
         downs = [(i, j) for i, _ in rows for j in range(nb) if j < i]
         cur = {(i, j): xs[j] for i, j in downs}
         for k in range(max((i - j for i, j in downs), default=0)):
             live = [(i, j) for i, j in downs if k < i - j]
             outs = _run_convbn_seqs([self.fuse_layers[i][j][k] for i, j in live],
-                                    [cur[ij] for ij in live])
+                                    [cur[ij] for ij in live],
+                                    [links[j] if k == 0 else None for _, j in live])
             cur.update(zip(live, outs))
         terms.update(cur)
         out = []
         for i, _ in rows:
             out.append(ops.fuse_sum_relu([xs[j] if j == i else terms[(i, j)] for j in range(nb)],
-                                         xs[i].shape[1:3]))
+                                         xs[i].shape[1:3],
+                                         [links[i] if j == i else None for j in range(nb)]))
         return out
 
 

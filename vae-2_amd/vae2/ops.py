@@ -739,7 +739,7 @@ def _up_bwd(g, shape):
 
 class _FuseSum(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, out_hw, *terms):
+    def forward(ctx, out_hw, links, *terms):
         ref = terms[0]
         n, c = ref.shape[0], ref.shape[3]
         y = new_act((n, out_hw[0], out_hw[1], c), ref)
@@ -752,6 +752,7 @@ class _FuseSum(torch.autograd.Function):
         yp, ya = act_of(y)
         call("vae2_fuse_sum_relu", len(terms), ptrs, acts, yp, ctypes.byref(ya), stream_ptr())
         ctx.shapes = [tuple(t.shape) for t in terms]
+        ctx.links = links
         ctx.save_for_backward(y)
         return y
 
@@ -763,22 +764,41 @@ class _FuseSum(torch.autograd.Function):
         dyp, dya = act_of(dy)
         yp, ya = act_of(y)
         gp, ga = act_of(g)
-        call("vae2_relu_bwd", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), gp, ctypes.byref(ga),
-             stream_ptr())
+        links = ctx.links or (None,) * len(ctx.shapes)
+        lk = next((i for i, l in enumerate(links) if l is not None), None)
+        if lk is not None and ctx.needs_input_grad[lk + 2]:
+            # the identity term's input has other consumers (ops.GradLink): its share of
+            # the gradient goes straight into (or onto) their shared buffer
+            link = links[lk]
+            beta = 0.0
+            if link.buf is None:
+                link.buf = new_act(tuple(y.shape), y)
+            else:
+                beta = 1.0
+            bp, ba = act_of(link.buf)
+            call("vae2_relu_bwd_dual", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), gp,
+                 ctypes.byref(ga), bp, ctypes.byref(ba), beta, stream_ptr())
+        else:
+            lk = None
+            call("vae2_relu_bwd", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), gp,
+                 ctypes.byref(ga), stream_ptr())
         grads = []
         for i, shp in enumerate(ctx.shapes):
-            if not ctx.needs_input_grad[i + 1]:
+            if not ctx.needs_input_grad[i + 2]:
                 grads.append(None)
+            elif i == lk:
+                grads.append(links[i].finish())
             elif shp[1:3] == tuple(y.shape[1:3]):
                 grads.append(g)
             else:
                 grads.append(_up_bwd(g, shp))
-        return (None, *grads)
+        return (None, None, *grads)
 
 
-def fuse_sum_relu(terms, out_hw):
-    """relu(sum of terms), lower-resolution terms bilinearly upsampled to out_hw."""
-    return _FuseSum.apply(tuple(out_hw), *terms)
+def fuse_sum_relu(terms, out_hw, links=None):
+    """relu(sum of terms), lower-resolution terms bilinearly upsampled to out_hw.  links:
+    per term an ops.GradLink (or None) shared with the term's other consumers."""
+    return _FuseSum.apply(tuple(out_hw), tuple(links) if links else None, *terms)
 
 
 class _UpCat(torch.autograd.Function):
