@@ -681,9 +681,13 @@ def _bn_layer(x, a, o, dy, dres, save, gamma, part, sums_p, countp, count, relu)
                         _p(save), _p(gamma), _p(part), sums_p, countp, float(count), int(relu))
 
 
+BN_BATCH = True  # False: conv_bn_multi runs its layers one by one (A/B and parity tests)
+
+
 def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=None):
     """[conv_bn(xs[i], convs[i], bns[i], relu, residuals[i], ...)] for independent layers,
-    their BatchNorm steps batched into shared launches (training mode)."""
+    their BatchNorm steps batched into shared launches (training mode; with SyncBN one
+    statistics exchange per direction for all of them)."""
     n = len(xs)
     residuals = residuals if residuals is not None else [None] * n
     x_links = x_links if x_links is not None else [None] * n
@@ -694,7 +698,7 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
         spec = ConvSpec(convs[i], bns[i], relus[i])
         spec.x_link, spec.res_link = x_links[i], res_links[i]
         specs.append(spec)
-    if (not all(sp.training for sp in specs) or
+    if (not BN_BATCH or not all(sp.training for sp in specs) or
             not all(r is None or _bn_quad_ok(r) for r in residuals)):
         return [conv_bn(xs[i], convs[i], bns[i], relus[i], residuals[i], x_links[i],
                         res_links[i]) for i in range(n)]
