@@ -440,23 +440,39 @@ __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
     const int qs = Q - q0 < p.cs4 ? Q - q0 : p.cs4;
     // ---- stage the halo tile of this slab (zero outside the image / past a_c) ----
     __syncthreads();
-    const int total = LH * LW * qs;
-    for (int i = threadIdx.x; i < total; i += 256) {
-      const int pix = i / qs;
-      const int q = i - pix * qs;
-      const int lr = pix / LW, lc = pix - lr * LW;
-      const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
-      const bool ok = (unsigned)ih < (unsigned)p.img_h && (unsigned)iw < (unsigned)p.img_w;
-      const int c = (q0 + q) * 4;
-      const uint32_t off =
-          ok ? (uint32_t)(((img_base + ih) * p.img_w + iw) * p.a_ps + c) * 4u : kOOB;
-      f4 v = load4(arsrc, off);
-      if (c + 4 > p.a_c) {
+    // thread -> (channel quad q = tid % qs, pixels pb, pb + pstride, ...); SB loads in
+    // flight per thread before their LDS stores (few round trips, few extra registers)
+    constexpr int SB = 3;
+    {
+    const int sq = threadIdx.x % qs, pb = threadIdx.x / qs, pstride = 256 / qs;
+    const int c = (q0 + sq) * 4;
+    const bool cpad = c + 4 > p.a_c;
+    if (pb < pstride) {
+      for (int pix0 = pb; pix0 < LH * LW; pix0 += SB * pstride) {
+        f4 v[SB];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (c + k >= p.a_c) v[k] = 0.f;
+        for (int u = 0; u < SB; ++u) {
+          const int pix = pix0 + u * pstride;
+          const int lr = pix / LW, lc = pix - lr * LW;
+          const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
+          const bool ok = pix < LH * LW && (unsigned)ih < (unsigned)p.img_h &&
+                          (unsigned)iw < (unsigned)p.img_w;
+          v[u] = load4(arsrc, ok ? (uint32_t)(((img_base + ih) * p.img_w + iw) * p.a_ps + c) * 4u
+                                 : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const int pix = pix0 + u * pstride;
+          if (pix >= LH * LW) break;
+          if (cpad) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (c + k >= p.a_c) v[u][k] = 0.f;
+          }
+          *reinterpret_cast<f4*>(&tile[pix * csp + 4 * sq]) = v[u];
+        }
       }
-      *reinterpret_cast<f4*>(&tile[pix * csp + 4 * q]) = v;
+    }
     }
     __syncthreads();
     // ---- 9 taps x qs quads of K from LDS ----

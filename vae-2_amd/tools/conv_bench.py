@@ -62,6 +62,8 @@ def timeit(fn, iters):
 
 
 def main():
+    if os.environ.get("VAE2_LIB"):  # A/B runs against another build of the library
+        _lib.LIB_PATH = os.environ["VAE2_LIB"]
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
