@@ -310,6 +310,80 @@ def test_conv_bn_train(relu, res, stride, cout):
     assert int(bn_g.num_batches_tracked) == int(bn_c.num_batches_tracked) == 1
 
 
+KS_SHAPES = [
+    # N, H, W, Cin, Cout, k, stride: the gather kernel's in-workgroup K split (KS = 4:
+    # >= 16 K chunks and < 512 workgroups), its BN-statistics epilogue, and stride-2
+    # data gradients (parity classes, some with no valid tap) accumulated with beta = 1
+    (2, 8, 8, 144, 144, 3, 1),
+    (1, 16, 16, 144, 72, 3, 2),
+    (2, 6, 10, 72, 144, 3, 2),
+    (4, 4, 4, 270, 144, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", KS_SHAPES)
+@pytest.mark.parametrize("ksplit", [True, False])
+def test_igemm_ksplit_conv_bn_and_accumulating_dgrad(shape, ksplit):
+    """conv_bn (training) through the gather kernel with the K split on and off
+    (vae2_conv2d_set_algo bit 8): output, BN running statistics (the KS epilogue's
+    per-tile rows), input / weight / BN gradients against PyTorch; then the data
+    gradient accumulated onto a prefilled buffer (beta = 1, the GradLink path)."""
+    import ctypes
+    from vae2 import _lib, ops
+    torch.manual_seed(2)
+    n, h, w, cin, cout, k, s = shape
+    pad = k // 2
+    conv = nn.Conv2d(cin, cout, k, s, pad, bias=False)
+    bn = nn.BatchNorm2d(cout, momentum=0.01)
+    nn.init.normal_(bn.weight, 1.0, 0.2)
+    nn.init.normal_(bn.bias, 0.0, 0.2)
+    conv_g = nn.Conv2d(cin, cout, k, s, pad, bias=False).to(DEV)
+    conv_g.load_state_dict(conv.state_dict())
+    bn_g = nn.BatchNorm2d(cout, momentum=0.01).to(DEV)
+    bn_g.load_state_dict(bn.state_dict())
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    y_ref = F.relu(bn(conv(x)))
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    lib = _lib.load()
+    prev = lib.vae2_conv2d_set_algo(1 | (0 if ksplit else 8))
+    try:
+        xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+        with torch.no_grad():
+            xg.copy_(nhwc(x.detach()).to(DEV))
+        xg.requires_grad_(True)
+        yg = ops.conv_bn(xg, conv_g, bn_g, relu=True)
+        yg.backward(nhwc(gy).to(DEV))
+        torch.cuda.synchronize()
+        assert rel(nchw(yg), y_ref) < TOL
+        assert rel(nchw(xg.grad), x.grad) < 1e-4
+        assert rel(conv_g.weight.grad, conv.weight.grad) < 1e-4
+        assert rel(bn_g.weight.grad, bn.weight.grad) < 1e-4
+        assert rel(bn_g.bias.grad, bn.bias.grad) < 1e-5
+        assert rel(bn_g.running_mean, bn.running_mean) < 1e-5
+        assert rel(bn_g.running_var, bn.running_var) < 1e-5
+        # data gradient onto a prefilled buffer (beta = 1)
+        oh, ow = y_ref.shape[2:]
+        dyc = torch.randn(n, cout, oh, ow)
+        pre = torch.randn(n, cin, h, w)
+        xr = torch.zeros(n, cin, h, w, requires_grad=True)
+        F.conv2d(xr, conv.weight.detach(), None, s, pad).backward(dyc)
+        dy = ops.new_act((n, oh, ow, cout), xg)
+        dx = ops.new_act((n, h, w, cin), xg)
+        with torch.no_grad():
+            dy.copy_(nhwc(dyc).to(DEV))
+            dx.copy_(nhwc(pre).to(DEV))
+        dyp, dya = ops.act_of(dy)
+        dxp, dxa = ops.act_of(dx)
+        wp = ops.packed_weight(conv_g.weight, 1)
+        ops.call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ops.ptr(wp), dxp,
+                 ctypes.byref(dxa), k, s, pad, 1.0, ops.stream_ptr())
+        torch.cuda.synchronize()
+        assert rel(nchw(dx), xr.grad + pre) < TOL
+    finally:
+        lib.vae2_conv2d_set_algo(prev)
+
+
 def test_conv_bn_eval():
     from vae2 import ops
     torch.manual_seed(2)
