@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 5
+#define VAE2_ABI_VERSION 6
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -348,6 +348,20 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
 int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n,
                                      float* const* dxs, const vae2_act* dxds, float* ws,
                                      int64_t ws_size, void* stream);
+
+/* dxs[s] = adj(dy) + betas[s]*dxs[s] (betas may be NULL: 0) for n <= 3 targets whose h
+ * and w are dy's divided by the same 2, 4 or 8 (any order): the HighResolutionModule
+ * fuse backward (enc_hrnet.py:233-249, the lower branches' upsample terms of one output
+ * row), thread per (pixel, channel quad) for narrow channel counts.  _ws_size returns
+ * the workspace in floats, or -1 when a target is not such a downsampling (callers
+ * then take vae2_upsample_bilinear_bwd per target).  dy and ws 16-byte aligned,
+ * dyd->ps % 4 == 0.                                                             */
+int64_t vae2_upsample_bilinear_bwd_pow2_ws_size(const vae2_act* dyd, int n,
+                                                const vae2_act* dxds);
+int vae2_upsample_bilinear_bwd_pow2(const float* dy, const vae2_act* dyd, int n,
+                                    float* const* dxs, const vae2_act* dxds,
+                                    const float* betas, float* ws, int64_t ws_size,
+                                    void* stream);
 
 /* g = dy * (y > 0)  (ReLU backward, threshold_backward).                       */
 int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,

@@ -422,11 +422,17 @@ def test_up_cat(shapes):
 
 
 @pytest.mark.parametrize("c,sizes", [(8, [(16, 12), (16, 12), (8, 6), (2, 2)]),
-                                     (18, [(16, 32), (8, 16), (2, 4), (1, 1)])])
-def test_fuse_sum_relu(c, sizes):
+                                     (18, [(16, 32), (8, 16), (2, 4), (1, 1)]),
+                                     (18, [(32, 64), (16, 32), (8, 16), (4, 8)]),
+                                     (36, [(16, 16), (8, 8), (4, 4)]),
+                                     (6, [(8, 16), (4, 8)])])
+@pytest.mark.parametrize("pow2", [True, False])
+def test_fuse_sum_relu(c, sizes, pow2, monkeypatch):
     """Includes 18 channels (a padded channel quad in the vectorised adjoint), x8
-    upsampling and a 1x1 source (a window wider than the adjoint's unrolled one)."""
+    upsampling and a 1x1 source (a window wider than the adjoint's unrolled one); the
+    exact 2/4/8 rows take vae2_upsample_bilinear_bwd_pow2 unless pow2 is off."""
     from vae2 import ops
+    monkeypatch.setattr(ops, "UP_POW2", pow2)
     torch.manual_seed(4)
     hw = sizes[0]
     terms = [torch.randn(2, c, h, w, requires_grad=True) for h, w in sizes]
@@ -442,6 +448,48 @@ def test_fuse_sum_relu(c, sizes):
     assert rel(nchw(yg), y_ref) < 1e-6
     for a, b in zip(tg, terms):
         assert rel(nchw(a.grad), b.grad) < 1e-5
+
+
+def test_upsample_bwd_pow2_betas_and_order():
+    """The ABI directly: targets in any ratio order, beta accumulation, 1-pixel targets
+    (both edge folds on one source), and -1 for a non power-of-two target."""
+    import ctypes
+    from vae2 import ops
+    from vae2._lib import Act, call, load
+    lib = load()
+    torch.manual_seed(6)
+    n, c, H, W = 2, 10, 8, 16
+    dy = torch.randn(n, c, H, W)
+    tshapes = [(2, 4), (8 // 2, 16 // 2), (1, 2)]  # ratios 4, 2, 8
+    ref, prev, betas = [], [], [0.0, 1.0, 0.5]
+    for (h, w), b in zip(tshapes, betas):
+        z = torch.zeros(n, c, h, w, requires_grad=True)
+        F.interpolate(z, size=[H, W], mode="bilinear").backward(dy)
+        p0 = torch.randn(n, c, h, w)
+        prev.append(p0)
+        ref.append(z.grad + b * p0)
+    g = ops.new_act((n, H, W, c), torch.empty(0, device=DEV))
+    g.copy_(nhwc(dy))
+    dxs = []
+    for p in prev:
+        d = ops.new_act(tuple(nhwc(p).shape), g)
+        d.copy_(nhwc(p))
+        dxs.append(d)
+    gp, ga = ops.act_of(g)
+    views = [ops.act_of(d) for d in dxs]
+    acts = (Act * 3)(*[a for _, a in views])
+    wsz = lib.vae2_upsample_bilinear_bwd_pow2_ws_size(ctypes.byref(ga), 3, acts)
+    assert wsz > 0
+    ws = torch.empty(wsz, device=DEV)
+    bt = (ctypes.c_float * 3)(*betas)
+    ptrs = (ctypes.c_void_p * 3)(*[p for p, _ in views])
+    call("vae2_upsample_bilinear_bwd_pow2", gp, ctypes.byref(ga), 3, ptrs, acts, bt,
+         ws.data_ptr(), wsz, None)
+    torch.cuda.synchronize()
+    for d, r in zip(dxs, ref):
+        assert rel(nchw(d), r) < 1e-6
+    bad = (Act * 1)(Act(n, 3, 5, c, c))
+    assert lib.vae2_upsample_bilinear_bwd_pow2_ws_size(ctypes.byref(ga), 1, bad) == -1
 
 
 def test_cat_codemap_and_avgpool():

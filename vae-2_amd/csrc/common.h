@@ -144,6 +144,15 @@ __device__ __forceinline__ float lerp_weight(int o, int in_size, float scale, in
   return w;
 }
 
+// Exact 2^k ratios (the HRNet branches of a power-of-two image): source column i of
+// a bilinear upsample by F receives the 2F output pixels F*i + d, d = -F/2 .. 3F/2-1,
+// with the hat weight 1 - |2d + 1 - F| / 2F (interpolate's lerp weights, exact in
+// fp32); at the image edges the forward's clamped tap lands on column 0 / w-1, i.e.
+// the virtual columns -1 and w are folded into them.  Same rule vertically.
+__device__ constexpr float hat_w(int d, int f) {
+  return 1.f - (float)(2 * d + 1 - f < 0 ? f - 1 - 2 * d : 2 * d + 1 - f) / (float)(2 * f);
+}
+
 // Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream);

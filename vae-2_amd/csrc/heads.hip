@@ -663,15 +663,7 @@ __global__ __launch_bounds__(256) void up_adj_v_kernel(UpAdj p, int s) {
   }
 }
 
-// Exact 2^(s+1) ratios (the HRNet branches of a power-of-two image): static stencils.
-// Source column i receives the 2F output pixels F*i + d, d = -F/2 .. 3F/2-1, with the hat
-// weight 1 - |2d + 1 - F| / 2F (interpolate's lerp weights, exact in fp32); at the image
-// edges the forward's clamped tap lands on column 0 / zw-1, i.e. the virtual columns -1
-// and zw are folded into them.  Same rule vertically.
-__device__ constexpr float hat_w(int d, int f) {
-  return 1.f - (float)(2 * d + 1 - f < 0 ? f - 1 - 2 * d : 2 * d + 1 - f) / (float)(2 * f);
-}
-
+// Exact 2^(s+1) ratios: static stencils (hat_w, common.h).
 constexpr int kAdjHalo = 4;  // F/2 for F <= 8
 
 // Horizontal pass, workgroup = (dY row, 64-pixel chunk, 64-channel block); the chunk and a

@@ -223,6 +223,80 @@ __global__ __launch_bounds__(256) void upsample_bwd4_kernel(const float* __restr
   }
 }
 
+// The adjoint for up to 3 targets at exact 2, 4, 8 ratios (a fuse row's lower branches),
+// one thread per (pixel, channel quad) so that narrow layers (18 channels) keep every
+// lane busy: a horizontal pass of all targets (one launch) into a quad-padded workspace
+// hb[s] = [n][H][zw][4Q], then a vertical pass of all targets (one launch), both with the
+// static hat stencils.  dy is read once from HBM; hb (1/F of dy each) twice from L2.
+struct UpAdjQ {
+  const float* g;
+  int64_t g_ps;
+  int H, W, Q, C, nt;
+  float* hb[3];
+  float* dx[3];
+  int64_t dx_ps[3];
+  int zh[3], zw[3], lf[3];  // lf = log2 of the ratio (1..3)
+  float beta[3];
+  uint32_t cnt_h[3], cnt_v[3];
+  FastDiv zwq[3], zh_d[3], q_d;
+};
+
+// sum_d hat_w(d, F) v[F*i + d] over a line of `len` points with stride `st`, edges folded.
+template <int F>
+__device__ __forceinline__ f4v hat_adj(const float* line, int64_t st, int len, int i, int n_src) {
+  constexpr int HF = F / 2;
+  const int x0 = F * i;
+  f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int d = -HF; d < 3 * HF; ++d) {
+    const int x = x0 + d;
+    if (x >= 0 && x < len) acc += hat_w(d, F) * *reinterpret_cast<const f4v*>(line + x * st);
+  }
+  if (i == 0) {  // virtual source -1: points d - F
+#pragma unroll
+    for (int d = F; d < 3 * HF; ++d)
+      acc += hat_w(d, F) * *reinterpret_cast<const f4v*>(line + (d - F) * st);
+  }
+  if (i == n_src - 1) {  // virtual source n_src: points len + d
+#pragma unroll
+    for (int d = -HF; d < 0; ++d)
+      acc += hat_w(d, F) * *reinterpret_cast<const f4v*>(line + (len + d) * st);
+  }
+  return acc;
+}
+
+template <bool VERT>
+__global__ __launch_bounds__(256) void up_adjq_kernel(UpAdjQ p) {
+  const int s = blockIdx.y;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (VERT ? p.cnt_v[s] : p.cnt_h[s])) return;
+  const int zw = p.zw[s], Q = p.Q, lf = p.lf[s];
+  const uint32_t row = p.zwq[s].div(i);  // horizontal: n*H + oy; vertical: n*zh + iy
+  const uint32_t r = i - row * (uint32_t)(zw * Q);
+  const uint32_t ix = p.q_d.div(r);
+  const uint32_t q = r - ix * (uint32_t)Q;
+  const int64_t hrow = (int64_t)zw * 4 * Q;  // hb row stride
+  if (!VERT) {
+    const float* line = p.g + (int64_t)row * p.W * p.g_ps + 4 * q;
+    const f4v acc = lf == 1   ? hat_adj<2>(line, p.g_ps, p.W, (int)ix, zw)
+                    : lf == 2 ? hat_adj<4>(line, p.g_ps, p.W, (int)ix, zw)
+                              : hat_adj<8>(line, p.g_ps, p.W, (int)ix, zw);
+    *reinterpret_cast<f4v*>(p.hb[s] + (int64_t)row * hrow + 4 * (ix * Q + q)) = acc;
+    return;
+  }
+  const uint32_t n = p.zh_d[s].div(row);
+  const int iy = (int)(row - n * (uint32_t)p.zh[s]);
+  const float* line = p.hb[s] + (int64_t)n * p.H * hrow + 4 * (ix * Q + q);
+  const f4v acc = lf == 1   ? hat_adj<2>(line, hrow, p.H, iy, p.zh[s])
+                  : lf == 2 ? hat_adj<4>(line, hrow, p.H, iy, p.zh[s])
+                            : hat_adj<8>(line, hrow, p.H, iy, p.zh[s]);
+  float* dst = p.dx[s] + ((int64_t)row * zw + ix) * p.dx_ps[s] + 4 * q;
+  const float beta = p.beta[s];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if ((int)(4 * q) + k < p.C) dst[k] = (beta != 0.f) ? acc[k] + beta * dst[k] : acc[k];
+}
+
 struct FuseTerms {
   const float* x[4];
   Act d[4];
@@ -508,6 +582,68 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
                      as_stream(stream), dy, to_act(dyd), dx, to_act(dxd), beta,
                      FastDiv((uint32_t)dxd->c), FastDiv((uint32_t)dxd->w),
                      FastDiv((uint32_t)dxd->h));
+  return check_launch(fn);
+}
+
+// log2 of an exact power-of-two ratio in {2, 4, 8}, else 0.
+static int pow2_ratio(int64_t big, int64_t small) {
+  for (int k = 1; k <= 3; ++k)
+    if (big == small << k) return k;
+  return 0;
+}
+
+int64_t vae2_upsample_bilinear_bwd_pow2_ws_size(const vae2_act* dyd, int n,
+                                                const vae2_act* dxds) {
+  if (!act_ok(dyd) || n < 1 || n > 3 || !dxds) return -1;
+  const int64_t Q = (dyd->c + 3) / 4;
+  int64_t t = 0;
+  for (int s = 0; s < n; ++s) {
+    const vae2_act* d = &dxds[s];
+    const int k = pow2_ratio(dyd->w, d->w);
+    if (!act_ok(d) || !k || pow2_ratio(dyd->h, d->h) != k || d->n != dyd->n || d->c != dyd->c)
+      return -1;
+    t += dyd->n * dyd->h * d->w * 4 * Q;
+  }
+  return t;
+}
+
+int vae2_upsample_bilinear_bwd_pow2(const float* dy, const vae2_act* dyd, int n,
+                                    float* const* dxs, const vae2_act* dxds,
+                                    const float* betas, float* ws, int64_t ws_size,
+                                    void* stream) {
+  const char* fn = "vae2_upsample_bilinear_bwd_pow2";
+  VAE2_REQUIRE(dy && act_ok(dyd) && n >= 1 && n <= 3 && dxs && dxds && ws, fn,
+               "bad arguments");
+  const int64_t need = vae2_upsample_bilinear_bwd_pow2_ws_size(dyd, n, dxds);
+  VAE2_REQUIRE(need >= 0, fn, "targets are not exact 2 / 4 / 8 downsamplings of dy");
+  VAE2_REQUIRE(ws_size >= need, fn, "workspace too small");
+  VAE2_REQUIRE(dyd->ps % 4 == 0 && (uintptr_t)dy % 16 == 0 && (uintptr_t)ws % 16 == 0, fn,
+               "dy and ws must be 16-byte aligned with a pixel stride of 4k");
+  UpAdjQ p{};
+  p.g = dy; p.g_ps = dyd->ps; p.H = (int)dyd->h; p.W = (int)dyd->w; p.C = (int)dyd->c;
+  p.Q = (p.C + 3) / 4; p.nt = n; p.q_d = FastDiv((uint32_t)p.Q);
+  float* hb = ws;
+  uint32_t mh = 0, mv = 0;
+  for (int s = 0; s < n; ++s) {
+    const vae2_act* d = &dxds[s];
+    VAE2_REQUIRE(dxs[s], fn, "null target");
+    const int64_t ch = dyd->n * dyd->h * d->w * p.Q, cv = dyd->n * d->h * d->w * p.Q;
+    VAE2_REQUIRE(ch < (int64_t(1) << 31), fn, "tensor too large");
+    p.dx[s] = dxs[s]; p.dx_ps[s] = d->ps; p.zh[s] = (int)d->h; p.zw[s] = (int)d->w;
+    p.lf[s] = pow2_ratio(dyd->w, d->w);
+    p.beta[s] = betas ? betas[s] : 0.f;
+    p.cnt_h[s] = (uint32_t)ch; p.cnt_v[s] = (uint32_t)cv;
+    p.zwq[s] = FastDiv((uint32_t)(d->w * p.Q)); p.zh_d[s] = FastDiv((uint32_t)d->h);
+    p.hb[s] = hb;
+    hb += dyd->n * dyd->h * d->w * 4 * p.Q;
+    if (p.cnt_h[s] > mh) mh = p.cnt_h[s];
+    if (p.cnt_v[s] > mv) mv = p.cnt_v[s];
+  }
+  hipStream_t st = as_stream(stream);
+  VAE2_LAUNCH(up_adjq_kernel<false>, dim3((mh + 255) / 256, n), dim3(256), 0, st, p);
+  int rc = check_launch(fn);
+  if (rc) return rc;
+  VAE2_LAUNCH(up_adjq_kernel<true>, dim3((mv + 255) / 256, n), dim3(256), 0, st, p);
   return check_launch(fn);
 }
 

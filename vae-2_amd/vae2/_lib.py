@@ -76,7 +76,10 @@ _SIGS = {
     "vae2_upsample_bilinear_bwd_multi_ws_size": (c_i64, [P_ACT, c_int, P_ACT]),
     "vae2_upsample_bilinear_bwd_multi": (c_int, [c_vp, P_ACT, c_int, ctypes.POINTER(c_vp), P_ACT,
                                                  c_vp, c_i64, c_vp]),
-    "vae2_head_out_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp]),
+    "vae2_upsample_bilinear_bwd_pow2_ws_size": (c_i64, [P_ACT, c_int, P_ACT]),
+    "vae2_upsample_bilinear_bwd_pow2": (c_int, [c_vp, P_ACT, c_int, ctypes.POINTER(c_vp), P_ACT,
+                                                c_vp, c_vp, c_i64, c_vp]),
+    "vae2_head_out_fwd":(c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp]),
     "vae2_head_out_bwd_ws_size": (c_i64, [P_ACT, c_int]),
     "vae2_head_out_bwd_reduce": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_int, c_vp, P_ACT, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
@@ -140,7 +143,7 @@ _SIGS = {
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lib = None
 
 

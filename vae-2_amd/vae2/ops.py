@@ -741,6 +741,29 @@ def _up_bwd(g, shape):
     return dx
 
 
+UP_POW2 = True  # the fuse rows' lower-branch adjoints in two launches (exact 2/4/8 ratios)
+
+
+def _up_bwd_pow2(g, shapes):
+    """Adjoints of up to 3 upsample terms at once (vae2_upsample_bilinear_bwd_pow2), or
+    None when the ratios are not exact powers of two (callers take _up_bwd per term)."""
+    if not UP_POW2 or len(shapes) > 3:
+        return None
+    lib = _lib.load()
+    gp, ga = act_of(g)
+    dxs = [new_act(shp, g) for shp in shapes]
+    views = [act_of(d) for d in dxs]
+    acts = (Act * len(dxs))(*[a for _, a in views])
+    wsz = lib.vae2_upsample_bilinear_bwd_pow2_ws_size(ctypes.byref(ga), len(dxs), acts)
+    if wsz < 0 or ga.ps % 4 or g.data_ptr() % 16:
+        return None
+    ptrs = (ctypes.c_void_p * len(dxs))(*[p for p, _ in views])
+    ws = _empty((max(wsz, 1),), g)
+    call("vae2_upsample_bilinear_bwd_pow2", gp, ctypes.byref(ga), len(dxs), ptrs, acts, None,
+         ptr(ws), wsz, stream_ptr())
+    return dxs
+
+
 class _FuseSum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, out_hw, links, *terms):
@@ -787,6 +810,9 @@ class _FuseSum(torch.autograd.Function):
             call("vae2_relu_bwd", dyp, ctypes.byref(dya), yp, ctypes.byref(ya), gp,
                  ctypes.byref(ga), stream_ptr())
         grads = []
+        ups = [i for i, shp in enumerate(ctx.shapes)
+               if ctx.needs_input_grad[i + 2] and i != lk and shp[1:3] != tuple(y.shape[1:3])]
+        upg = _up_bwd_pow2(g, [ctx.shapes[i] for i in ups]) if ups else None
         for i, shp in enumerate(ctx.shapes):
             if not ctx.needs_input_grad[i + 2]:
                 grads.append(None)
@@ -794,6 +820,8 @@ class _FuseSum(torch.autograd.Function):
                 grads.append(links[i].finish())
             elif shp[1:3] == tuple(y.shape[1:3]):
                 grads.append(g)
+            elif upg is not None:
+                grads.append(upg[ups.index(i)])
             else:
                 grads.append(_up_bwd(g, shp))
         return (None, None, *grads)
