@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 6
+#define VAE2_ABI_VERSION 7
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -449,6 +449,45 @@ int vae2_weighted_sum(int n, const float* const* terms, const float* lambdas,
  * utils.py:63-65). x is a dense array of n floats.                              */
 int vae2_nonfinite_check(const float* x, int64_t n, int32_t* flag,
                          void* stream);
+
+/* ------------------------------------------------------------ clip input ---- */
+
+/* CityscapesSequence.input_transform + __getitem__ (cityscapes.py:311-326): a batch of
+ * uint8 RGB frame windows frames[n][nframes][h][w][3] (dense, 4-byte aligned) becomes
+ * nseg NCHW fp32 segment tensors outs[s][n][3*nframes/nseg][h][w], channel 3*f + rgb,
+ * value lut[rgb*256 + byte].  The caller tabulates the reference's per-element
+ * arithmetic ((byte/255 in fp32 - mean) / std in fp64, rounded to fp32: vae2/clips.py
+ * normalize_lut) as a [3][256] fp32 device table.  nseg in [1, 8], nseg | nframes.   */
+int vae2_clip_normalize_u8(const uint8_t* frames, int64_t n, int64_t nframes, int64_t h,
+                           int64_t w, const float* lut, int nseg, float* const* outs,
+                           void* stream);
+
+/* --------------------------------------------------------- eval metrics ---- */
+
+/* _to_image (function.py:86-97) over NCHW fp32 planes, RGB = channel % 3:
+ * y = clip((fp32(fp32(x * std) + mean)) * 255, 0, 255) (x*std and +mean in fp64 as
+ * numpy does for a float32 array against the fp64 mean/std arrays).  mean3 / std3 are
+ * HOST arrays.  y may alias x.                                                    */
+int vae2_to_image(const float* x, float* y, int64_t n, int64_t c, int64_t h, int64_t w,
+                  const double* mean3, const double* std3, void* stream);
+/* Workspace (doubles) for vae2_absdiff_sqdiff_sum / vae2_ssim over `planes` h x w
+ * planes.                                                                         */
+int64_t vae2_metrics_ws_size(int64_t planes, int64_t h, int64_t w);
+/* out[0] = sum |a - b|, out[1] = sum (a - b)^2 over n floats, in double (device out):
+ * the recon_loss (function.py:252) and PSNR (criterion.py:106-116) sums.          */
+int vae2_absdiff_sqdiff_sum(const float* a, const float* b, int64_t n, double* ws,
+                            double* out, void* stream);
+/* pytorch_msssim _ssim (restated from pytorch_msssim 1.0.0, used at function.py:244-251):
+ * per plane p of x, y ([planes][h][w] fp32, h, w >= 11): the 11-tap separable window
+ * `win` (valid filtering) gives mu, sigma; out[2p] = mean SSIM map, out[2p+1] = mean
+ * contrast-structure map, C1 = (K1*L)^2, C2 = (K2*L)^2.  Device out, double.       */
+int vae2_ssim(const float* x, const float* y, int64_t planes, int64_t h, int64_t w,
+              const float* win, int win_size, float c1, float c2, double* ws, double* out,
+              void* stream);
+/* F.avg_pool2d(kernel 2, stride 2, padding (h % 2, w % 2)) of each plane (the MS-SSIM
+ * level step): y is [planes][(h + 2*(h%2) - 2)/2 + 1][(w + 2*(w%2) - 2)/2 + 1].     */
+int vae2_avgpool2x2(const float* x, float* y, int64_t planes, int64_t h, int64_t w,
+                    void* stream);
 
 /* ------------------------------------------------------------ optimizer ---- */
 

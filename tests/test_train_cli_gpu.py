@@ -72,3 +72,54 @@ def test_train_cli_full_vae2_gan_step(tmp_path):
     assert os.path.isfile(os.path.join(out, "model_D_final_state.pth"))
     d_state = ckd["optimizer_D"]["state"]
     assert int(float(d_state[0]["step"])) == 2
+
+
+@pytest.mark.parametrize("cache", [True, False])
+def test_train_and_inference_cli_on_sequence_zips(tmp_path, cache):
+    """The Cityscapes sequence-zip data path end to end: tools/train.py on 4 zips
+    (uint8 cache + ClipLoader, or the drop-in CityscapesSequence through a DataLoader),
+    then tools/inference.py (prior sampling, eval metrics) from the saved checkpoint."""
+    import numpy as np
+    from PIL import Image
+    from clip_fixtures import write_dataset
+    from vae2 import clips
+    data = tmp_path / "data"
+    data.mkdir()
+    lp = write_dataset(str(data), 4, hw=(24, 48), seed=4)
+    opts = ["DATASET.ROOT", str(data), "DATASET.TRAIN_SET", lp, "MI355X.SYNTHETIC_DATA", "False",
+            "MI355X.CLIP_CACHE", str(cache), "MI355X.ELBO_ONLY", "True"]
+    out = _train(tmp_path, "TRAIN.END_EPOCH", "1", *opts)
+    ck = torch.load(os.path.join(out, "checkpoint_encdec.pth.tar"), map_location="cpu",
+                    weights_only=True)
+    assert ck["epoch"] == 1
+    assert int(float(ck["optimizer_encdec"]["state"][0]["step"])) == 2  # 4 clips / B=2
+    assert os.path.isdir(os.path.join(str(data), ".vae2_cache")) == cache
+
+    import inference  # vae-2_amd/tools/inference.py (tools/ is on sys.path after _train)
+    from config import config
+    config.defrost()
+    config.merge_from_file(YAML)
+    config.freeze()
+    res = inference.main(["--cfg", YAML, "OUTPUT_DIR", str(tmp_path / "output"),
+                          "LOG_DIR", str(tmp_path / "log"), "TRAIN.IMAGE_SIZE", "[64, 32]",
+                          "TRAIN.BATCH_SIZE_PER_GPU", "2", "TRAIN.RESUME", "True",
+                          "MI355X.EVAL_SAMPLES", "2", *opts])
+    assert [r[0] for r in res] == ["seq001", "seq003"]  # the last clip of each batch
+    vis = os.path.join(out, "vis", "epoch0", "seq001")
+    # ground-truth frames: to_image(normalise(u8)) truncated to uint8 is the window again
+    u8 = clips.decode_sequence(os.path.join(str(data), "seq001.zip"), (32, 64), first=20,
+                               count=9)
+    for k, tag in enumerate(("x1t", "x2t", "x3t")):
+        for i in range(3):
+            png = np.asarray(Image.open(os.path.join(vis, f"{tag}_{i}.png")))
+            assert np.abs(png.astype(int) - u8[3 * k + i].astype(int)).max() <= 1
+    per = dict(res[0][1])
+    for tag in ("x2t", "x3t"):
+        m = per[tag]
+        assert m.shape == (2, 3, 4)
+        assert np.isfinite(m[..., [0, 1, 3]]).all() and np.isnan(m[..., 2]).all()
+        assert ((m[..., 1] > -1) & (m[..., 1] <= 1)).all()
+        lines = open(os.path.join(vis, f"{tag}predict", f"{tag}_0_ssimloss.txt")).read().split()
+        assert len(lines) == 2 and abs(float(lines[1]) - m[1, 0, 1]) < 1e-6
+        pngs = [f for f in os.listdir(os.path.join(vis, f"{tag}predict")) if f.endswith(".png")]
+        assert len(pngs) == 2 * 3

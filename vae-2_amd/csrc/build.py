@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(os.path.dirname(HERE), "vae2")
 OUT = os.path.join(PKG, "libvae2_hip.so")
 BUILD = os.path.join(HERE, "build")
-SOURCES = ["conv.hip", "bn.hip", "resample.hip", "elbo.hip", "heads.hip"]
+SOURCES = ["conv.hip", "bn.hip", "resample.hip", "elbo.hip", "heads.hip", "clips.hip",
+           "metrics.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "vae2_hip.h")]
 ARCH = os.environ.get("VAE2_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

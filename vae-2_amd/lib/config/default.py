@@ -46,6 +46,9 @@ _SCHEMA = {
         "SYNTHETIC_DATA": False,  # Cityscapes-shaped Gaussian clips instead of the zip dataset
         "SYNTHETIC_CLIPS": 64,
         "ELBO_ONLY": False,       # no discriminators / D step (the ELBO step alone)
+        "CLIP_CACHE": True,       # zip clips: decode once to a uint8 cache, GPU normalisation
+        "CLIP_CACHE_DIR": "",     # default <DATASET.ROOT>/.vae2_cache/<list>_<H>x<W>
+        "EVAL_SAMPLES": 100,      # prior samples per clip in tools/inference.py (function.py:124)
     },
 }
 

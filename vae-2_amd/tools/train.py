@@ -15,8 +15,10 @@ checkpoints are written (the reference calls `.module` on a non-DDP model,
 train.py:322); epochs past END_EPOCH use the main loader when no
 DATASET.EXTRA_TRAIN_SET is given (the reference raises a NameError there);
 `MI355X.ELBO_ONLY True` drops the two discriminators (the ELBO step alone; the
-reference always builds them and runs the D step); the Cityscapes zip dataset is
-replaced by MI355X.SYNTHETIC_DATA clips when that switch is set.
+reference always builds them and runs the D step); the Cityscapes sequence zips are
+decoded once into a uint8 cache and normalised on the GPU (MI355X.CLIP_CACHE, default),
+or replaced by MI355X.SYNTHETIC_DATA clips when that switch is set; the dataset is given
+TRAIN.CLIP_LENGTH (the reference leaves CityscapesSequence at its default 3).
 """
 import argparse
 import os
@@ -28,12 +30,14 @@ import timeit
 import torch
 
 import _init_paths  # noqa: F401
+import datasets  # noqa: F401  (lib/datasets: the drop-in CityscapesSequence)
 import models  # noqa: F401
 from config import config, update_config
 from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
 from core.function import adversarial_train
 from utils.utils import FullModel_D, FullModel_encdec, create_logger
 
+from vae2 import clips
 from vae2 import dist as vdist
 from vae2.optim import FusedAdam
 from vae2.trainer import NullWriter, SyntheticClips
@@ -51,12 +55,51 @@ def parse_args(argv=None):
     return args
 
 
-def build_dataset(cfg):
+def build_loader(cfg, list_path, shuffle, device, logger=None, random_pos=True):
+    """(loader, number of clips) for one list file (train.py:113-140).
+
+    MI355X.SYNTHETIC_DATA: Gaussian clips.  Otherwise the Cityscapes sequence zips
+    (DATASET.ROOT + a list file, gen_cityscapes_data.py layout): with MI355X.CLIP_CACHE
+    decoded once into a uint8 cache (rank 0 builds it, the others wait) and served by
+    ClipLoader (pinned staging + HIP normalisation); without it the drop-in
+    CityscapesSequence through a torch DataLoader (PIL decode per item, uint8 windows
+    normalised on the GPU by adversarial_train)."""
+    w, h = cfg.TRAIN.IMAGE_SIZE
+    B = cfg.TRAIN.BATCH_SIZE_PER_GPU
     if cfg.MI355X.SYNTHETIC_DATA:
-        w, h = cfg.TRAIN.IMAGE_SIZE
-        return SyntheticClips(cfg.MI355X.SYNTHETIC_CLIPS, cfg.TRAIN.CLIP_LENGTH, h, w)
-    raise NotImplementedError(
-        "the Cityscapes zip clip dataset is SURVEY.md §8f next-2; set MI355X.SYNTHETIC_DATA True")
+        dataset = SyntheticClips(cfg.MI355X.SYNTHETIC_CLIPS, cfg.TRAIN.CLIP_LENGTH, h, w)
+    elif cfg.DATASET.DATASET != "cityscapessequence":
+        raise ValueError("VAE2 trains on DATASET.DATASET cityscapessequence (got {})"
+                         .format(cfg.DATASET.DATASET))
+    elif cfg.MI355X.CLIP_CACHE:
+        cdir = cfg.MI355X.CLIP_CACHE_DIR or clips.cache_dir_for(cfg.DATASET.ROOT, list_path,
+                                                                (h, w))
+        if vdist.rank() == 0:
+            clips.build_cache(cfg.DATASET.ROOT, list_path, (h, w), cache_dir=cdir,
+                              log=logger.info if logger else None)
+        if vdist.is_dist():
+            torch.distributed.barrier()
+        cache = clips.ClipCache(cdir)
+        sampler = (torch.utils.data.distributed.DistributedSampler(range(len(cache)))
+                   if vdist.is_dist() else None)
+        loader = clips.ClipLoader(cache, B, clip_length=cfg.TRAIN.CLIP_LENGTH, clip_num=3,
+                                  sampler=sampler, shuffle=shuffle and sampler is None,
+                                  random_pos=random_pos, device=device)
+        return loader, sampler, len(cache)
+    else:
+        dataset = datasets.cityscapessequence(
+            root=cfg.DATASET.ROOT, list_path=list_path, num_samples=None,
+            num_classes=cfg.DATASET.NUM_CLASSES, multi_scale=cfg.TRAIN.MULTI_SCALE,
+            flip=cfg.TRAIN.FLIP, ignore_label=cfg.TRAIN.IGNORE_LABEL,
+            base_size=cfg.TRAIN.BASE_SIZE, crop_size=(h, w),
+            downsample_rate=cfg.TRAIN.DOWNSAMPLERATE, scale_factor=cfg.TRAIN.SCALE_FACTOR,
+            clip_length=cfg.TRAIN.CLIP_LENGTH, random_pos=random_pos,
+            fixed_length=cfg.DATASET.FIXED_LENGTH)
+    sampler = torch.utils.data.distributed.DistributedSampler(dataset) if vdist.is_dist() else None
+    loader = torch.utils.data.DataLoader(
+        dataset, batch_size=B, shuffle=shuffle and sampler is None, num_workers=cfg.WORKERS,
+        pin_memory=True, drop_last=True, sampler=sampler)
+    return loader, sampler, len(dataset)
 
 
 def main(argv=None):
@@ -98,12 +141,12 @@ def main(argv=None):
     device = torch.device("cuda:{}".format(args.local_rank))
     torch.cuda.set_device(device)
 
-    dataset = build_dataset(config)
-    sampler = torch.utils.data.distributed.DistributedSampler(dataset) if vdist.is_dist() else None
-    loader = torch.utils.data.DataLoader(
-        dataset, batch_size=config.TRAIN.BATCH_SIZE_PER_GPU,
-        shuffle=config.TRAIN.SHUFFLE and sampler is None, num_workers=config.WORKERS,
-        pin_memory=True, drop_last=True, sampler=sampler)
+    loader, sampler, n_clips = build_loader(config, config.DATASET.TRAIN_SET,
+                                            config.TRAIN.SHUFFLE, device, logger)
+    extra_loader, extra_sampler = loader, sampler
+    if config.DATASET.EXTRA_TRAIN_SET:  # train.py:142-167
+        extra_loader, extra_sampler, _ = build_loader(config, config.DATASET.EXTRA_TRAIN_SET,
+                                                      config.TRAIN.SHUFFLE, device, logger)
 
     model_encdec = FullModel_encdec(
         encz_model=encz_model, encdec_model=encdec_model, D_model_sequence=D_model_sequence,
@@ -129,7 +172,7 @@ def main(argv=None):
             for f in (opt.flats if opt is not None else []):
                 torch.distributed.broadcast(f.data, src=0)
 
-    epoch_iters = int(len(dataset) / config.TRAIN.BATCH_SIZE_PER_GPU / max(1, len(gpus)))
+    epoch_iters = int(n_clips / config.TRAIN.BATCH_SIZE_PER_GPU / max(1, len(gpus)))
     last_epoch = 0
     state_file = os.path.join(final_output_dir, "checkpoint_encdec.pth.tar")
     state_file_D = os.path.join(final_output_dir, "checkpoint_D.pth.tar")
@@ -154,9 +197,11 @@ def main(argv=None):
     for epoch in range(last_epoch, end_epoch):
         if sampler is not None:
             sampler.set_epoch(epoch)
+        if extra_sampler is not None and extra_sampler is not sampler:
+            extra_sampler.set_epoch(epoch)
         if epoch >= config.TRAIN.END_EPOCH:  # extra epochs restart the schedule (train.py:300-306)
             ep_args = (epoch - config.TRAIN.END_EPOCH, config.TRAIN.EXTRA_EPOCH, epoch_iters,
-                       config.TRAIN.EXTRA_LR, extra_iters, loader)
+                       config.TRAIN.EXTRA_LR, extra_iters, extra_loader)
             for opt in (optimizer, optimizer_D):
                 if opt is not None:
                     opt.set_lr(config.TRAIN.EXTRA_LR)

@@ -141,9 +141,18 @@ _SIGS = {
     "vae2_adam_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                                c_i64, c_vp]),
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
+    "vae2_clip_normalize_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int,
+                                       ctypes.POINTER(c_vp), c_vp]),
+    "vae2_to_image": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
+                              ctypes.POINTER(c_f64), ctypes.POINTER(c_f64), c_vp]),
+    "vae2_metrics_ws_size": (c_i64, [c_i64, c_i64, c_i64]),
+    "vae2_absdiff_sqdiff_sum": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "vae2_ssim": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
+                          c_vp, c_vp]),
+    "vae2_avgpool2x2": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lib = None
 
 

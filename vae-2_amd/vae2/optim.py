@@ -8,7 +8,6 @@ graph and replayed (vae2.graph.StepGraph); change the learning rate through
 param_groups[0]["lr"] and the next eager step() — or set_lr() between replays.  state_dict() / load_state_dict() use torch.optim.Adam's format
 (per-parameter exp_avg / exp_avg_sq / step) so optimizer checkpoints interchange.
 """
-import ctypes
 
 import torch
 
@@ -116,6 +115,3 @@ class FusedAdam:
         self.eps = g.get("eps", self.eps)
         self.weight_decay = g.get("weight_decay", self.weight_decay)
 
-
-def _unused():  # keep ctypes imported for type checkers of call sites
-    return ctypes

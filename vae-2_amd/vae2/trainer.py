@@ -6,7 +6,7 @@
                       parameters), meters, PRINT_FREQ logging.
   SyntheticClips      Cityscapes-shaped clips (3 segments x CLIP_LENGTH RGB frames
                       stacked on channels, cityscapes.py:311-326) for
-                      benchmarking and CI; the zip/PNG dataset is next-2.
+                      benchmarking and CI; the zip/PNG clips are vae2/clips.py.
   create_logger, AverageMeter, get_world_size, get_rank   (utils.py)
 """
 import logging
@@ -17,6 +17,7 @@ from pathlib import Path
 
 import torch
 
+from . import clips
 from . import dist as vdist
 
 
@@ -124,10 +125,7 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
     flats = optimizer_encdec.flats
     for i_iter, batch in enumerate(trainloader):
         xs, name = batch
-        assert len(xs) == 3
-        xt = xs[0].to(device)
-        x2t = xs[1].to(device)
-        x3t = xs[2].to(device)
+        xt, x2t, x3t = clips.batch_to_device(xs, device)  # uint8 windows: HIP normalisation
         losses, xt_predict, x2t_predict, x3t_predict = model_encdec(
             xt=xt, x2t=x2t, x3t=x3t, multiplier=multiplier, is_baseline=is_baseline,
             baseline_mode=baseline_mode)
