@@ -340,6 +340,11 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
 int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
                        float* y, const vae2_act* yd, void* stream);
 
+/* Head-kernel variants (A/B measurement): bit 0 = the per-channel-lane vertical pass of
+ * the power-of-two upsampling adjoint instead of the row-streaming one.  Returns the
+ * previous setting.  Process-wide.                                                 */
+int vae2_heads_set_algo(int algo);
+
 /* dxs[s] = adjoint of bilinear_up (align_corners=False) applied to dy, for n <= 3
  * lower-resolution targets at once, reading dy once (separable: a horizontal pass into
  * the workspace, then a vertical pass per target).  dxs[s] have dy's channel count.  */

@@ -125,3 +125,31 @@ def test_heads_packed_cols_follow_optimizer_updates():
         got = vheads.run(hip_h, ys_d).permute(0, 3, 1, 2).cpu()
         want = ref_heads(ref_h, [y.double() for y in ys])
     assert max_rel(got, want) < 1e-5, max_rel(got, want)
+
+
+@pytest.mark.parametrize("hw,n", [((64, 128), 2), ((32, 64), 3)])
+def test_upsample_adjoint_streaming_equals_lane_kernel(hw, n):
+    """The row-streaming vertical pass of the power-of-two upsampling adjoint
+    (up_adj2_vs_kernel) against the per-channel-lane one (vae2_heads_set_algo bit 0):
+    same weights, same summation order."""
+    from vae2 import _lib
+    from vae2 import heads as vheads
+    heads, ys = _heads_and_inputs("w18", hw, n)
+    gout = None
+    grads = []
+    lib = _lib.load()
+    try:
+        for algo in (0, 1):
+            lib.vae2_heads_set_algo(algo)
+            hip_h = [copy.deepcopy(h).to(DEV) for h in heads]
+            ys_hip = [y.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_() for y in ys]
+            out = vheads.run(hip_h, ys_hip)
+            if gout is None:
+                gout = torch.randn(out.shape, generator=torch.Generator().manual_seed(3)).to(DEV)
+            out.backward(gout)
+            torch.cuda.synchronize()
+            grads.append([y.grad.cpu() for y in ys_hip])
+    finally:
+        lib.vae2_heads_set_algo(0)
+    for a, b in zip(*grads):
+        assert max_rel(a, b) < 1e-6, max_rel(a, b)

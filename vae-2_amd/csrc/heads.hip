@@ -313,7 +313,11 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
 // unconditional buffer loads, source columns clamped into the chunk's window), and the
 // epilogue adds the two horizontal taps per source and the bias, stores y and
 // accumulates the BN partial sums (written once per workgroup).
-constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32, kUsVS = 68;  // VS: LDS column stride
+constexpr int kUsXB = 64, kUsCB = 64, kUsMaxCin = 32;
+// LDS column stride of source s's blended row: the epilogue's 4 lane groups read columns
+// 2 (s = 0), 1 (s = 1) or 0-1 (s = 2) apart, so stride * step = 16 (mod 32) puts each
+// 32-lane half of a ds_read_b32 on distinct banks.
+__host__ __device__ constexpr int us_vs(int s) { return s == 0 ? 72 : 80; }
 constexpr int kUsRows = 8;                                          // image rows per workgroup
 
 struct UpSum {
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   extern __shared__ __attribute__((aligned(16))) float usm[];
   __shared__ double red[2][4][kUsCB];
   f4* tab = reinterpret_cast<f4*>(usm);                  // [NUP][kUsXB] {i0, i1, l0, l1}
-  float* vs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // [sum_s vcols_s][kUsVS]
+  float* vs = usm + 4 * (NUP > 0 ? NUP : 1) * kUsXB;     // per source [vcols_s][us_vs(s)]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -373,12 +377,12 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   for (int s = 0; s < NUP; ++s) {
     vlo[s] = lerp_index(x0, p.zw[s], p.sw[s]).i0;
     vhi[s] = lerp_index(x0 + xn - 1, p.zw[s], p.sw[s]).i1;
-    voff[s] = s == 0 ? 0 : voff[s - 1] + p.vcols[s - 1];
+    voff[s] = s == 0 ? 0 : voff[s - 1] + p.vcols[s - 1] * us_vs(s - 1);  // floats
     if (threadIdx.x < xn) {
       const Lerp lx = lerp_index(x0 + threadIdx.x, p.zw[s], p.sw[s]);
       tab[s * kUsXB + threadIdx.x] =
-          f4{__int_as_float((voff[s] + lx.i0 - vlo[s]) * kUsVS),
-             __int_as_float((voff[s] + lx.i1 - vlo[s]) * kUsVS), lx.l0, lx.l1};
+          f4{__int_as_float(voff[s] + (lx.i0 - vlo[s]) * us_vs(s)),
+             __int_as_float(voff[s] + (lx.i1 - vlo[s]) * us_vs(s)), lx.l0, lx.l1};
     }
   }
   float bj[4];
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
       for (int u = 0; u < VU; ++u) {
         const int j = wave + 4 * u;  // uniform per wave
         if (vlo[s] + j <= vhi[s])
-          vs[(voff[s] + j) * kUsVS + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
+          vs[voff[s] + j * us_vs(s) + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
       }
     }
     // ---- W0 x0: acc[j][e] = pixel 16*wave + 4g + e, channel c0 + 16j + r ----
@@ -771,7 +775,61 @@ __global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
   }
 }
 
-// Pixels per block of the backward passes (<= 1024 blocks, >= 64 pixels each).
+// Streaming form of the vertical pass: it only mixes hb rows, and an hb row
+// (zw * C floats, ix-major) is contiguous, so thread = 4 consecutive floats of the row:
+// one 16-byte load per contributing row (2F taps, plus the edge folds on the first / last
+// target row: uniform per workgroup), the same weights and summation order as
+// up_adj2_v_kernel, then the 4 results go to (ix, c) = divmod(k, C) of the (possibly
+// channel-padded) dx layout.  Workgroup = (target row, slice of the row).  Needs
+// zw * C % 4 == 0 (16-byte aligned rows).
+static int g_adj_stream = 1;  // vae2_heads_set_algo bit 0 clears it
+
+template <int S>
+__global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) {
+  constexpr int F = 2 << S, HF = 1 << S;
+  const int row = blockIdx.x;  // n*zh + iy
+  const int zh = p.zh[S], zw = p.zw[S];
+  const int n = row / zh, iy = row - n * zh;
+  const int64_t rs = (int64_t)zw * p.C;
+  const int nq = (int)(rs >> 2);
+  const float* hb = p.hb[S] + (int64_t)n * p.H * rs;
+  float* out = p.dx[S] + (int64_t)row * zw * p.dx_ps[S];
+  const int oy0 = F * iy;
+  const uint32_t C = (uint32_t)p.C, dps = (uint32_t)p.dx_ps[S];
+  for (int q = blockIdx.y * 256 + threadIdx.x; q < nq; q += gridDim.y * 256) {
+    const int64_t k4 = 4 * (int64_t)q;
+    f4 v[4 * HF];
+#pragma unroll
+    for (int d = -HF; d < 3 * HF; ++d) {
+      const int oy = oy0 + d;
+      v[d + HF] = (oy >= 0 && oy < p.H) ? *reinterpret_cast<const f4*>(hb + oy * rs + k4)
+                                        : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = -HF; d < 3 * HF; ++d) acc += hat_w(d, F) * v[d + HF];
+    if (iy == 0) {
+#pragma unroll
+      for (int e = 0; e < HF; ++e)
+        acc += hat_w(F + e, F) * *reinterpret_cast<const f4*>(hb + e * rs + k4);
+    }
+    if (iy == zh - 1) {
+#pragma unroll
+      for (int e = 0; e < HF; ++e)
+        acc += hat_w(e - HF, F) *
+               *reinterpret_cast<const f4*>(hb + (int64_t)(F * zh - HF + e) * rs + k4);
+    }
+    uint32_t ix = cdiv.div((uint32_t)k4), c = (uint32_t)k4 - ix * C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[(int64_t)ix * dps + c] = acc[i];
+      if (++c == C) { c = 0; ++ix; }
+    }
+  }
+}
+
+// Pixels per block of the backward passes (<= 1024 blocks, >= 64 pixels each).  (2048
+// blocks with 8 pixels in flight per thread measured slower: the partial rows double.)
 static int64_t head_ppb(int64_t P) {
   int64_t ppb = ceil_div(P, 1024);
   return ppb < 64 ? 64 : ppb;
@@ -912,7 +970,7 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
     p.sw[s] = (float)u->w / (float)yd->w;
     p.vcols[s] = (int)ceilf(p.sw[s] * kUsXB) + 3;
     VAE2_REQUIRE(p.vcols[s] <= 48, fn, "source wider than half the output (upsampling only)");
-    vtot += p.vcols[s];
+    vtot += p.vcols[s] * us_vs(s);
   }
   p.y = y; p.y_bytes = (uint32_t)y_bytes; p.C = (int)yd->c;
   p.stats = stats;
@@ -920,8 +978,7 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   p.nrb = (int)ceil_div(yd->h, kUsRows);
   p.rows = (int)vae2_conv1x1_upsum_stats_rows(yd);
   const int nu = nup > 0 ? nup : 1;
-  const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1) * kUsVS) *
-                     sizeof(float);
+  const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1)) * sizeof(float);
   dim3 grid((unsigned)(yd->n * p.nrb * p.nxb * ncb));
   hipStream_t st = as_stream(stream);
   switch (nup) {
@@ -939,6 +996,12 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
   int64_t t = 0;
   for (int s = 0; s < n; ++s) t += dyd->n * dyd->h * dxds[s].w * dyd->c;
   return t > 0 ? t : 1;
+}
+
+int vae2_heads_set_algo(int algo) {
+  const int prev = g_adj_stream ? 0 : 1;
+  g_adj_stream = (algo & 1) ? 0 : 1;
+  return prev;
 }
 
 int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n,
@@ -982,11 +1045,23 @@ int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n
     int rc = check_launch(fn);
     if (rc) return rc;
     for (int s = 0; s < n; ++s) {
-      const dim3 gv((unsigned)(dyd->n * p.zh[s]), cb);
-      switch (s) {
-        case 0: VAE2_LAUNCH(up_adj2_v_kernel<0>, gv, dim3(256), 0, st, p); break;
-        case 1: VAE2_LAUNCH(up_adj2_v_kernel<1>, gv, dim3(256), 0, st, p); break;
-        default: VAE2_LAUNCH(up_adj2_v_kernel<2>, gv, dim3(256), 0, st, p); break;
+      const int64_t rs = (int64_t)p.zw[s] * p.C;
+      if (rs % 4 == 0 && g_adj_stream) {
+        const int64_t nq = rs / 4;
+        const dim3 gv((unsigned)(dyd->n * p.zh[s]), (unsigned)ceil_div(nq, 512));
+        const FastDiv cdiv((uint32_t)p.C);
+        switch (s) {
+          case 0: VAE2_LAUNCH(up_adj2_vs_kernel<0>, gv, dim3(256), 0, st, p, cdiv); break;
+          case 1: VAE2_LAUNCH(up_adj2_vs_kernel<1>, gv, dim3(256), 0, st, p, cdiv); break;
+          default: VAE2_LAUNCH(up_adj2_vs_kernel<2>, gv, dim3(256), 0, st, p, cdiv); break;
+        }
+      } else {
+        const dim3 gv((unsigned)(dyd->n * p.zh[s]), cb);
+        switch (s) {
+          case 0: VAE2_LAUNCH(up_adj2_v_kernel<0>, gv, dim3(256), 0, st, p); break;
+          case 1: VAE2_LAUNCH(up_adj2_v_kernel<1>, gv, dim3(256), 0, st, p); break;
+          default: VAE2_LAUNCH(up_adj2_v_kernel<2>, gv, dim3(256), 0, st, p); break;
+        }
       }
       rc = check_launch(fn);
       if (rc) return rc;

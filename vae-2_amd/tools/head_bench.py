@@ -82,6 +82,9 @@ def main():
         call("vae2_upsample_bilinear_bwd_multi", ynp, ctypes.byref(yna), 3, gptrs, gacts, ptr(uws),
              usz, s)
     res.append(("upsample adjoint x3 (dy read + dx write)", timeit(adj, a.iters), P * C * 4 + zb))
+    lib.vae2_heads_set_algo(1)
+    res.append(("  same, per-channel-lane vertical pass", timeit(adj, a.iters), P * C * 4 + zb))
+    lib.vae2_heads_set_algo(0)
 
     save = torch.cat([torch.zeros(C), torch.ones(C), torch.ones(C), torch.zeros(C)]).to(dev)
     w2 = torch.randn(3, C, device=dev)

@@ -150,6 +150,7 @@ _SIGS = {
     "vae2_ssim": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
                           c_vp, c_vp]),
     "vae2_avgpool2x2": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "vae2_heads_set_algo": (c_int, [c_int]),
 }
 
 ABI_VERSION = 7
