@@ -1,0 +1,105 @@
+"""The data-parallel path over RCCL itself (the "nccl" backend), on the one GPU of a
+test box: a world-size-1 RCCL process group with the distributed code paths forced on
+(vae2.dist.is_dist patched), so every SyncBN exchange (batched per BN depth level, Σx /
+Σx² doubles + counts), the bucketed gradient all-reduce + 1/world scaling and the loss
+reduce run as real RCCL collectives on device buffers, issued from the posterior net's
+side stream as in the 8-GPU runs.  With one rank the collectives are identities, so
+the step must reproduce the non-distributed step exactly (the reference's golden loss
+within 1e-5 as well).  Multi-rank numerics are covered by test_dist_gpu.py (gloo, 2
+ranks on one GPU; RCCL refuses two ranks per device)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from test_dist_gpu import ROOT, _port
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(dev, g, fm_cls, build, make_cfg, t, FusedAdam):
+    ed, ez = build(make_cfg("tiny"))
+    fm = fm_cls(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(dev)
+    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-4)
+    fm.set_noise(t(g["eps"]), t(g["code"]))
+    opt.zero_grad()
+    losses, _, x2p, x3p = fm(t(g["xt"]).to(dev), t(g["x2t"]).to(dev), t(g["x3t"]).to(dev), 1.0)
+    losses[0].backward()
+    return fm, opt, losses[0], x2p, x3p
+
+
+def _work(port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from helpers import build, golden, make_cfg, t
+    from vae2 import dist as vdist
+    from vae2.model import FullModel_encdec
+    from vae2.optim import FusedAdam
+    dev = "cuda:0"
+    torch.cuda.set_device(0)
+    g = golden("tiny_native")
+    # reference run: no process group
+    _, opt0, l0, x20, x30 = _step(dev, g, FullModel_encdec, build, make_cfg, t, FusedAdam)
+    torch.cuda.synchronize()
+    ref = (float(l0), x20.detach().cpu().numpy(),
+           torch.cat([f.grad for f in opt0.flats]).double().cpu())
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    assert dist.get_backend() == "nccl"
+    vdist.is_dist = lambda: True
+    vdist.set_sync_bn(True)
+    calls = [0]
+    orig = vdist.all_reduce_
+
+    def counting(t_, group=None):
+        calls[0] += 1
+        return orig(t_, group=group)
+    vdist.all_reduce_ = counting
+    fm, opt, loss, x2p, _ = _step(dev, g, FullModel_encdec, build, make_cfg, t, FusedAdam)
+    exchanges = calls[0]
+    vdist.allreduce_grads(opt.flats)
+    red = vdist.reduce_tensor(loss.detach().clone())
+    torch.cuda.synchronize()
+    got = (float(loss), x2p.detach().cpu().numpy(),
+           torch.cat([f.grad for f in opt.flats]).double().cpu())
+    opt.step()
+    torch.cuda.synchronize()
+    fwd_same = got[0] == ref[0] and np.array_equal(got[1], ref[1])
+    grad_rel = float((got[2] - ref[2]).norm() / ref[2].norm())
+    q.put(("ok", got[0], float(red), float(g["loss_loss_all"]), fwd_same, grad_rel, exchanges))
+    dist.destroy_process_group()
+
+
+def _worker(port, q):
+    try:
+        _work(port, q)
+    except BaseException:
+        import traceback
+        q.put(("error", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.timeout(300)
+def test_rccl_world1_dist_path_equals_single_process_step():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), q))
+    p.start()
+    import queue
+    try:
+        res = q.get(timeout=240)
+    except queue.Empty:
+        p.kill()
+        pytest.fail(f"RCCL run did not report (exit code {p.exitcode})")
+    p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, loss, reduced, ref, fwd_same, grad_rel, exchanges = res
+    assert abs(loss - ref) <= 1e-5 * abs(ref)
+    assert reduced == loss
+    assert exchanges > 50  # SyncBN statistics went through RCCL
+    assert fwd_same, "the RCCL path changed the forward"
+    assert grad_rel < 1e-5, grad_rel  # GradLink accumulation order only
