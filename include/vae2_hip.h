@@ -76,6 +76,29 @@ int vae2_conv2d_set_mfma_bf16(int on);
 int vae2_wgrad_defer(int on);
 int vae2_wgrad_flush(void* stream);
 
+/* Independent convolutions in one call (the lock-stepped layers of one HRNet depth
+ * level).  Each job is one vae2_conv2d_fwd (kind 0: x, xd -> y, yd with bias, beta,
+ * stats) or vae2_conv2d_bwd_data (kind 1: x, xd = dy -> y, yd = dx with beta; bias and
+ * stats ignored) call with the same meaning; jobs the LDS-tiled direct 3x3 kernel
+ * takes share launches (up to 4 per launch, grouped by tile shape; jobs writing the
+ * same output never share one), the others are issued one by one.  The jobs must be
+ * independent (no job reads another's output).  Grouping is off by default (measured
+ * slower in the full training step, where side-stream concurrency already fills the
+ * chip); vae2_conv2d_set_grouping(1) enables it; returns the previous setting.       */
+typedef struct vae2_conv_job {
+  int32_t kind, k, stride, pad;
+  const float* x;
+  vae2_act xd;
+  const float* wp;
+  const float* bias;
+  float* y;
+  vae2_act yd;
+  float beta;
+  float* stats;
+} vae2_conv_job;
+int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream);
+int vae2_conv2d_set_grouping(int on);
+
 /* Conv weights are consumed in a packed layout (zero-padded, K = (tap, 4-channel
  * quad) ordered): mode 0 for vae2_conv2d_fwd  = [round_up(Cout,64)][k*k][round_up(Cin,4)],
  * mode 1 for vae2_conv2d_bwd_data = [round_up(Cin,64)][k*k][round_up(Cout,4)].

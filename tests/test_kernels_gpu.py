@@ -564,3 +564,106 @@ def test_fused_adam_matches_torch():
     ref_sd = opt_ref.state_dict()
     for k in ref_sd["state"]:
         assert rel(sd["state"][k]["exp_avg"], ref_sd["state"][k]["exp_avg"]) < 1e-6
+
+
+MULTI_SHAPES = [
+    # N, H, W, Cin, Cout, k, bias: one depth level's independent convs
+    (2, 16, 32, 18, 18, 3, False),
+    (2, 13, 40, 36, 36, 3, True),
+    (1, 8, 32, 154, 144, 3, False),
+    (2, 5, 7, 3, 5, 3, False),
+    (2, 16, 32, 18, 18, 3, True),
+    (2, 8, 8, 36, 18, 1, False),   # 1x1: not a direct-3x3 job, issued on its own
+    (2, 13, 40, 36, 36, 3, False),
+]
+
+
+def test_conv2d_multi_grouped_equals_single_calls():
+    """vae2_conv2d_multi (direct-3x3 jobs sharing launches, grouped by tile shape) gives
+    the single-call results bit for bit: forward outputs and BN partial statistics, and
+    data gradients, including two data-gradient jobs accumulating into one output
+    (beta 0 then 1: the second runs after the first's launch)."""
+    import ctypes
+    from vae2 import _lib, ops
+    from vae2._lib import Act
+    lib = _lib.load()
+    prev = lib.vae2_conv2d_set_algo(2)
+    prev_g = lib.vae2_conv2d_set_grouping(1)
+    s = ops.stream_ptr()
+    torch.manual_seed(5)
+    like = torch.empty(1, device=DEV)
+
+    class Spec:
+        def __init__(self, k):
+            self.k, self.stride, self.pad = k, 1, k // 2
+    try:
+        L = []
+        for (n, h, w, cin, cout, k, bias) in MULTI_SHAPES:
+            x = ops.new_act((n, h, w, cin), like).normal_()
+            dy = ops.new_act((n, h, w, cout), like).normal_()
+            wt = torch.randn(cout, cin, k, k, device=DEV) * 0.1
+            b = torch.randn(cout, device=DEV) if bias else None
+            xp, xa = ops.act_of(x)
+            rows = lib.vae2_conv2d_fwd_stats_rows(xp, ctypes.byref(xa),
+                                                  ctypes.byref(Act(n, h, w, cout, cout)), k, 1,
+                                                  k // 2)
+            L.append(dict(x=x, dy=dy, w=wt, b=b, k=k, rows=rows, shape=(n, h, w, cin, cout),
+                          w0=ops.packed_weight(wt, 0), w1=ops.packed_weight(wt, 1)))
+
+        def run(grouped):
+            outs, stats, dxs = [], [], []
+            cg = ops.ConvGroup() if grouped else None
+            for d in L:
+                n, h, w, cin, cout = d["shape"]
+                y = ops.new_act((n, h, w, cout), like)
+                st = torch.empty(2 * d["rows"] * cout, device=DEV)
+                xp, xa = ops.act_of(d["x"])
+                yp, ya = ops.act_of(y)
+                if grouped:
+                    cg.add(0, xp, xa, d["w0"], d["b"], yp, ya, Spec(d["k"]), 0.0, st)
+                else:
+                    _lib.call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ops.ptr(d["w0"]),
+                              ops.ptr(d["b"]), yp, ctypes.byref(ya), d["k"], 1, d["k"] // 2,
+                              0.0, ops.ptr(st), s)
+                outs.append(y)
+                stats.append(st)
+            if grouped:
+                cg.flush()
+            shared = None
+            for i, d in enumerate(L):
+                n, h, w, cin, cout = d["shape"]
+                # layers 0 and 4 have the same input shape: both write one dx (beta 0, 1)
+                if i == 4:
+                    dx, beta = shared, 1.0
+                else:
+                    dx, beta = ops.new_act((n, h, w, cin), like), 0.0
+                    if i == 0:
+                        shared = dx
+                dyp, dya = ops.act_of(d["dy"])
+                dxp, dxa = ops.act_of(dx)
+                if grouped:
+                    cg.add(1, dyp, dya, d["w1"], None, dxp, dxa, Spec(d["k"]), beta)
+                else:
+                    _lib.call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ops.ptr(d["w1"]),
+                              dxp, ctypes.byref(dxa), d["k"], 1, d["k"] // 2, beta, s)
+                dxs.append(dx)
+            if grouped:
+                cg.flush()
+            torch.cuda.synchronize()
+            return outs, stats, dxs
+
+        a = run(False)
+        lib.vae2_kernel_log(1)
+        b = run(True)
+        buf = ctypes.create_string_buffer(1 << 14)
+        lib.vae2_kernel_log_read(buf, len(buf))
+        lib.vae2_kernel_log(0)
+        names = buf.value.decode().split(";")
+    finally:
+        lib.vae2_conv2d_set_algo(prev)
+        lib.vae2_conv2d_set_grouping(prev_g)
+    assert any(nm.startswith("dconv3_group_kernel") for nm in names), names
+    assert len(names) < 2 * len(MULTI_SHAPES), names  # fewer launches than jobs
+    for ta, tb in zip(a, b):
+        for u, v in zip(ta, tb):
+            assert torch.equal(u, v)

@@ -474,3 +474,40 @@ def test_deferred_nonfinite_check_raises():
         fm(xt.to(DEV), t(g["x2t"]).to(DEV), t(g["x3t"]).to(DEV), 1.0)
     with pytest.raises(AssertionError, match="nan or inf"):
         fm.check_anomalies()
+
+
+def test_bench_geometry_grouped_convs_are_exact():
+    """At the benchmark's geometry (128x256, B=8: the lower branches' direct-3x3 convs
+    share launches per depth level) the training step with grouped conv launches equals
+    the step with every conv on its own launch bit for bit (loss, predictions, every
+    gradient)."""
+    from vae2 import _lib
+    from vae2.model import FullModel_encdec
+    from vae2.optim import FusedAdam
+    lib = _lib.load()
+    gen = torch.Generator().manual_seed(4)
+    xs = [torch.randn(8, 9, 128, 256, generator=gen).to(DEV) for _ in range(3)]
+    eps = torch.randn(8, 10, 1, 1, generator=gen)
+    code = torch.randn(8, 10, 1, 1, generator=gen)
+    out = []
+    prev = lib.vae2_conv2d_set_grouping(1)
+    try:
+        for on in (1, 0):
+            lib.vae2_conv2d_set_grouping(on)
+            ed, ez = build(make_cfg(arch="w18", hw=(128, 256)))
+            fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0,
+                                  0.0).to(DEV)
+            opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-4)
+            fm.set_noise(eps, code)
+            opt.zero_grad()
+            losses, _, x2p, _ = fm(*xs, 1.0)
+            losses[0].backward()
+            torch.cuda.synchronize()
+            out.append((float(losses[0]), x2p.detach().cpu(),
+                        torch.cat([f.grad for f in opt.flats]).cpu()))
+    finally:
+        lib.vae2_conv2d_set_grouping(prev)
+    (l1, p1, g1), (l0, p0, g0) = out
+    assert l1 == l0
+    assert torch.equal(p1, p0)
+    assert torch.equal(g1, g0)

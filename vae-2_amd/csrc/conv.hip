@@ -388,21 +388,22 @@ struct DConv {
 constexpr int kDcBW = 32;     // tile columns
 constexpr int kDcMaxCs4 = 8;  // quads per slab
 
-template <int TM, int TN, bool FLIP, bool BF = false>
-__global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
+// One output tile: bm = tile index (image-major), by = N block, nrows = tiles of the
+// layer (rows of its BN partial statistics).
+template <int TM, int TN, bool FLIP, bool BF>
+__device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const int by,
+                                            const int nrows, float* __restrict__ tile) {
   constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
-  extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ float red[4][2][BN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
-  const int bm = xcd_remap(blockIdx.x, gridDim.x);
   const int per_img = p.tiles_h * p.tiles_w;
   const int img = bm / per_img;
   const int trem = bm - img * per_img;
   const int th = trem / p.tiles_w;
   const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * kDcBW;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = by * BN;
   const int kk4 = 9 * p.a_c4;
   const int csp = p.cs4 * 4 + 4;  // LDS floats per pixel (+4: bank spread)
   const int Q = p.a_c4 >> 2;
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
       }
     }
     __syncthreads();
-    const int rows = gridDim.x;
+    const int rows = nrows;
     for (int c = threadIdx.x; c < BN; c += 256) {
       if (n0 + c >= p.n) continue;
       float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
@@ -572,6 +573,40 @@ __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
       p.stats[(rows + bm) * p.n + n0 + c] = s2;
     }
   }
+}
+
+template <int TM, int TN, bool FLIP, bool BF = false>
+__global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  dconv3_body<TM, TN, FLIP, BF>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
+                                tile);
+}
+
+// Up to kDcGroup independent layers with the same tile shape in one launch (the lock-
+// stepped HRNet branches of one depth level: the low-resolution ones alone leave most
+// of the chip idle).  The 1-D grid is the concatenation of each layer's (tiles x N
+// blocks); the XCD remap runs over the whole grid, then the block finds its layer.
+constexpr int kDcGroup = 4;
+struct DConvGroup {
+  DConv p[kDcGroup];
+  int start[kDcGroup + 1];
+  int tiles[kDcGroup];
+  int n;
+};
+
+template <int TM, int TN, bool FLIP, bool BF = false>
+__global__ __launch_bounds__(256) void dconv3_group_kernel(DConvGroup gp) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);
+  int j = 0;
+#pragma unroll
+  for (int k = 1; k < kDcGroup; ++k) j += (k < gp.n && idx >= gp.start[k]) ? 1 : 0;
+  const DConv p = j == 0 ? gp.p[0] : j == 1 ? gp.p[1] : j == 2 ? gp.p[2] : gp.p[3];
+  const int t = j == 0 ? gp.tiles[0] : j == 1 ? gp.tiles[1] : j == 2 ? gp.tiles[2] : gp.tiles[3];
+  const int st = j == 0 ? gp.start[0] : j == 1 ? gp.start[1] : j == 2 ? gp.start[2] : gp.start[3];
+  const int local = idx - st;
+  const int by = local / t;
+  dconv3_body<TM, TN, FLIP, BF>(p, local - by * t, by, t, tile);
 }
 
 // ------------------------------------------------------------ tiling ----
@@ -1312,6 +1347,37 @@ static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipSt
   }
 }
 
+static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, const float* wp,
+                        uint32_t w_bytes, const float* bias, float* y, const vae2_act* yd,
+                        float beta, float* stats) {
+  DConv p{};
+  p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
+  p.img_h = (int)ad->h; p.img_w = (int)ad->w;
+  p.tiles_h = d.tiles_h; p.tiles_w = d.tiles_w; p.cs4 = d.cs4;
+  p.w = wp; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
+  p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
+  p.stats = stats;
+  return p;
+}
+
+static size_t dconv_shm(const DTile& d) {
+  return (size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) * sizeof(float);
+}
+
+template <int TM, bool FLIP>
+static void dconv_group_launch_tn(const DConvGroup& g, int tn, dim3 grid, size_t shm,
+                                  hipStream_t s) {
+  switch (tn) {
+#define CASE(T)                                                                          \
+  case T:                                                                                \
+    if (g_bf16) VAE2_LAUNCH((dconv3_group_kernel<TM, T, FLIP, true>), grid, dim3(256), shm, s, g); \
+    else VAE2_LAUNCH((dconv3_group_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, g);    \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+  }
+}
+
 static int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                         const float* bias, float* y, const vae2_act* yd, float beta,
                         float* stats, bool flip, hipStream_t s, const char* fn) {
@@ -1628,6 +1694,106 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
     p.y_offh = c.y_offh; p.y_offw = c.y_offw;
   }
   return launch_igemm(p, 1, as_stream(stream), fn, ncls);
+}
+
+// Independent convolutions in one call (one HRNet depth level): the jobs the direct 3x3
+// kernel takes are launched together, up to kDcGroup per launch, grouped by tile shape
+// and direction (jobs writing the same output never share a launch); the others go
+// through vae2_conv2d_fwd / vae2_conv2d_bwd_data one by one.
+static int g_conv_group = 0;  // measured slower in the full step: off by default
+
+int vae2_conv2d_set_grouping(int on) {
+  const int prev = g_conv_group;
+  g_conv_group = on ? 1 : 0;
+  return prev;
+}
+
+int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
+  const char* fn = "vae2_conv2d_multi";
+  VAE2_REQUIRE(n >= 0 && (n == 0 || jobs), fn, "bad arguments");
+  hipStream_t s = as_stream(stream);
+  struct Bucket {
+    int tm, tn, flip, cnt, tot;
+    DConvGroup g;
+    size_t shm;
+    const float* outs[kDcGroup];
+  };
+  Bucket b[8];
+  int nb = 0;
+  auto flush = [&](Bucket& k) -> int {
+    if (k.cnt == 0) return 0;
+    k.g.n = k.cnt;
+    k.g.start[k.cnt] = k.tot;
+    for (int q = k.cnt; q < kDcGroup; ++q) { k.g.start[q + 1] = k.tot; k.g.tiles[q] = 1; }
+    const dim3 grid((unsigned)k.tot);
+    if (k.tm == 4) {
+      if (k.flip) dconv_group_launch_tn<4, true>(k.g, k.tn, grid, k.shm, s);
+      else dconv_group_launch_tn<4, false>(k.g, k.tn, grid, k.shm, s);
+    } else {
+      if (k.flip) dconv_group_launch_tn<2, true>(k.g, k.tn, grid, k.shm, s);
+      else dconv_group_launch_tn<2, false>(k.g, k.tn, grid, k.shm, s);
+    }
+    k.cnt = 0; k.tot = 0; k.shm = 0;
+    return check_launch(fn);
+  };
+  // a job writing an output some queued job also writes runs after that job's launch
+  auto flush_holding = [&](const float* out) -> int {
+    for (int k = 0; k < nb; ++k)
+      for (int q = 0; q < b[k].cnt; ++q)
+        if (b[k].outs[q] == out) return flush(b[k]);
+    return 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    const vae2_conv_job& J = jobs[i];
+    VAE2_REQUIRE(J.kind == 0 || J.kind == 1, fn, "job kind must be 0 (forward) or 1 (data grad)");
+    if (int rc = flush_holding(J.y)) return rc;
+    const bool fwd = J.kind == 0;
+    const vae2_act* ad = &J.xd;  // the kernel's input: x (forward) or dy (data gradient)
+    const vae2_act* od = &J.yd;
+    bool direct = g_conv_group && J.x && J.wp && J.y &&
+                  (fwd ? conv_shapes_ok(ad, od, J.k, J.stride, J.pad)
+                       : conv_shapes_ok(od, ad, J.k, J.stride, J.pad)) &&
+                  fits32(ad) && fits32(od) && dconv_use(ad, od, J.k, J.stride, J.pad, J.x);
+    if (!direct) {
+      int rc = fwd ? vae2_conv2d_fwd(J.x, ad, J.wp, J.bias, J.y, od, J.k, J.stride, J.pad,
+                                     J.beta, J.stats, stream)
+                   : vae2_conv2d_bwd_data(J.x, ad, J.wp, J.y, od, J.k, J.stride, J.pad,
+                                          J.beta, stream);
+      if (rc) return rc;
+      continue;
+    }
+    const DTile d = pick_dtile(ad, od);
+    const uint32_t wb = (uint32_t)((fwd ? vae2_conv2d_packed_size(od->c, ad->c, J.k, 0)
+                                        : vae2_conv2d_packed_size(ad->c, od->c, J.k, 1)) * 4);
+    int k = 0;
+    while (k < nb && !(b[k].tm == d.tm && b[k].tn == d.tn && b[k].flip == (fwd ? 0 : 1))) ++k;
+    if (k == nb) {
+      VAE2_REQUIRE(nb < 8, fn, "too many tile shapes");
+      b[nb] = Bucket{};
+      b[nb].tm = d.tm; b[nb].tn = d.tn; b[nb].flip = fwd ? 0 : 1;
+      ++nb;
+    }
+    Bucket& B = b[k];
+    if (B.cnt == kDcGroup) {
+      int rc = flush(B);
+      if (rc) return rc;
+    }
+    const int tiles = (int)(ad->n * d.tiles_h * d.tiles_w);
+    B.g.p[B.cnt] = make_dconv(d, J.x, ad, J.wp, wb, fwd ? J.bias : nullptr, J.y, od, J.beta,
+                              fwd ? J.stats : nullptr);
+    B.g.start[B.cnt] = B.tot;
+    B.g.tiles[B.cnt] = tiles;
+    B.outs[B.cnt] = J.y;
+    B.tot += tiles * d.nblk;
+    const size_t sh = dconv_shm(d);
+    if (sh > B.shm) B.shm = sh;
+    ++B.cnt;
+  }
+  for (int k = 0; k < nb; ++k) {
+    int rc = flush(b[k]);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, int k) {

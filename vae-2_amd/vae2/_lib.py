@@ -151,6 +151,8 @@ _SIGS = {
                           c_vp, c_vp]),
     "vae2_avgpool2x2": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "vae2_heads_set_algo": (c_int, [c_int]),
+    "vae2_conv2d_multi": (c_int, [c_int, c_vp, c_vp]),
+    "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 
 ABI_VERSION = 7
@@ -187,6 +189,13 @@ class PackJob(ctypes.Structure):
     _fields_ = [("w", c_vp), ("out", c_vp), ("cout", ctypes.c_int32), ("cin", ctypes.c_int32),
                 ("k", ctypes.c_int32), ("mode", ctypes.c_int32), ("ld", ctypes.c_int32),
                 ("pad_", ctypes.c_int32)]
+
+
+class ConvJob(ctypes.Structure):
+    """vae2_conv_job (include/vae2_hip.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("stride", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("x", c_vp), ("xd", Act), ("wp", c_vp), ("bias", c_vp),
+                ("y", c_vp), ("yd", Act), ("beta", c_f32), ("stats", c_vp)]
 
 
 class HipError(RuntimeError):

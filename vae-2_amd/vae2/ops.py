@@ -294,6 +294,46 @@ def _conv_fwd(x, weight, bias, spec, stats=None):
     return y
 
 
+class ConvGroup:
+    """Independent convolutions of one depth level queued and issued by one
+    vae2_conv2d_multi call (direct-3x3 layers share launches).  Tensors a queued job
+    uses (packed weights) are held until the call is enqueued; `pending(t)` tells whether
+    a queued job writes t's storage (the caller flushes before touching it)."""
+
+    def __init__(self):
+        self.jobs, self.hold, self.outs = [], [], set()
+
+    def add(self, kind, x, xa, wp, bias, y, ya, spec, beta=0.0, stats=None):
+        self.jobs.append(_lib.ConvJob(kind, spec.k, spec.stride, spec.pad, x, xa, ptr(wp),
+                                      ptr(bias), y, ya, beta, ptr(stats)))
+        self.hold.append((wp, bias, stats))
+        self.outs.add(y.value if isinstance(y, ctypes.c_void_p) else int(y))
+
+    def pending(self, t):
+        return t is not None and t.data_ptr() in self.outs
+
+    def flush(self):
+        if not self.jobs:
+            return
+        arr = (_lib.ConvJob * len(self.jobs))(*self.jobs)
+        call("vae2_conv2d_multi", len(self.jobs), arr, stream_ptr())
+        self.jobs, self.hold, self.outs = [], [], set()
+
+
+def _conv_fwd_queued(group, x, weight, bias, spec, stats):
+    """_conv_fwd, queued on a ConvGroup."""
+    xp, xa = act_of(x)
+    n, h, w, _ = x.shape
+    oh, ow = spec.out_hw(h, w)
+    cout = weight.shape[0]
+    y = new_act((n, oh, ow, cout), x)
+    yp, ya = act_of(y)
+    if prof.active():
+        _conv_work("fwd", xa, (n, oh, ow, cout), spec.k, spec.stride)
+    group.add(0, xp, xa, packed_weight(weight, 0), bias, yp, ya, spec, 0.0, stats)
+    return y
+
+
 _WGRAD_BATCH = [0]  # open wgrad_batch contexts
 _WS_HOLD = []       # workspaces of queued weight-gradient reductions
 
@@ -319,8 +359,9 @@ class wgrad_batch:
         return False
 
 
-def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
-    """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b)."""
+def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, group=None):
+    """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b).  With a
+    ConvGroup the data gradient is queued on it (dx is complete once it is flushed)."""
     s = stream_ptr()
     xp, xa = act_of(x)
     dyp, dya = act_of(dy)
@@ -352,8 +393,11 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True):
         wp = packed_weight(weight, 1)
         if prof.active():
             _conv_work("dgrad", xa, tuple(dy.shape), spec.k, spec.stride)
-        call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp, ctypes.byref(dxa),
-             spec.k, spec.stride, spec.pad, beta, s)
+        if group is not None:
+            group.add(1, dyp, dya, wp, None, dxp, dxa, spec, beta)
+        else:
+            call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp,
+                 ctypes.byref(dxa), spec.k, spec.stride, spec.pad, beta, s)
         if link is not None:
             dx = link.finish()
     return dx, wret, bret
@@ -523,6 +567,7 @@ class _ConvBNMulti(torch.autograd.Function):
         L = [flat[6 * i:6 * i + 6] for i in range(n)]
         group = _bn_group()
         rs, saves, fins, counts, cs = [], [], [], [], []
+        cg = ConvGroup()
         for (x, weight, bias, gamma, beta, residual), spec in zip(L, specs):
             nn_, h, w, _ = x.shape
             oh, ow = spec.out_hw(h, w)
@@ -532,11 +577,12 @@ class _ConvBNMulti(torch.autograd.Function):
                                                   ctypes.byref(Act(nn_, oh, ow, cout, cout)),
                                                   spec.k, spec.stride, spec.pad)
             stats = _empty((2 * rows * cout,), x)
-            rs.append(_conv_fwd(x, weight, bias, spec, stats))
+            rs.append(_conv_fwd_queued(cg, x, weight, bias, spec, stats))
             saves.append(_empty((4 * cout,), x))
             counts.append(float(nn_ * oh * ow))
             cs.append(cout)
             fins.append((stats, rows))
+        cg.flush()  # the level's convs: direct-3x3 layers share launches
         tot = 2 * sum(cs)
         buf = _empty((tot + n,), rs[0], torch.float64)
         world = 1
@@ -643,6 +689,7 @@ class _ConvBNMulti(torch.autograd.Function):
                              for r, h_, d in zip(rs, ctx.has_res, dress)))
         call("vae2_bn_multi_bwd_apply", n, lay, s)
         grads = [None]
+        cg = ConvGroup()  # the level's data gradients: direct-3x3 layers share launches
         with wgrad_batch():  # the level's weight-gradient reductions in one launch
             for i in range(n):
                 spec = specs[i]
@@ -654,11 +701,15 @@ class _ConvBNMulti(torch.autograd.Function):
                     if link.buf is None:
                         link.buf = dres
                     else:
+                        if cg.pending(link.buf):
+                            cg.flush()
                         link.buf.add_(dres)
                     dres = link.finish()
                 dx, wret, bret_conv = _conv_bwd(x, weight, bias, drs[i], spec, need[1 + 6 * i],
-                                                need[1 + 6 * i + 1], need[1 + 6 * i + 2])
+                                                need[1 + 6 * i + 1], need[1 + 6 * i + 2],
+                                                group=cg)
                 grads += [dx, wret, bret_conv, gret, bret, dres]
+            cg.flush()
         return tuple(grads)
 
 

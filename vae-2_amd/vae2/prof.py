@@ -26,8 +26,8 @@ _ACTIVE = None
 
 # (family, regex on a kernel name), first match wins (also used by tools/trace_steps.py)
 FAMILIES = (
-    ("conv_fwd", r"dconv3_kernel<\d+, \d+, false|igemm_kernel<\d+, \d+, \w+, 0"),
-    ("conv_dgrad", r"dconv3_kernel<\d+, \d+, true|igemm_kernel<\d+, \d+, \w+, [12]"),
+    ("conv_fwd", r"dconv3_(group_)?kernel<\d+, \d+, false|igemm_kernel<\d+, \d+, \w+, 0"),
+    ("conv_dgrad", r"dconv3_(group_)?kernel<\d+, \d+, true|igemm_kernel<\d+, \d+, \w+, [12]"),
     ("conv_wgrad", r"wgrad"),
     ("batchnorm", r"bn_|reduce_then|chan_partials|partials_reduce"),
     ("heads", r"upsum|head_|up_adj"),
@@ -63,8 +63,13 @@ def active():
 
 
 def note(flops=0.0, nbytes=0.0, shape=None):
-    """Annotate the next C-ABI call with its algorithmic work (no-op unless profiling)."""
+    """Annotate the next C-ABI call with its algorithmic work (no-op unless profiling);
+    several notes before one call (a grouped launch) add up, their shapes joined by ' + '."""
     if _ACTIVE is not None:
+        if _ACTIVE.pending is not None:
+            f0, b0, s0 = _ACTIVE.pending
+            shape = s0 if shape is None else (shape if s0 is None else f"{s0} + {shape}")
+            flops, nbytes = f0 + flops, b0 + nbytes
         _ACTIVE.pending = (float(flops), float(nbytes), shape)
 
 
