@@ -79,8 +79,9 @@ def parse():
     ap.add_argument("--conv-grouping", choices=("on", "off"), default="off",
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="replay the step as one captured HIP graph (auto = off: the eager "
-                         "step, whose side streams overlap, measured 2-3%% faster)")
+                    help="replay the step as one captured HIP graph (auto: at N=1).  The "
+                         "eager step measured 0-3%% faster on an idle host but 10-20%% "
+                         "slower when the host CPUs are busy; the graph replay is stable")
     return ap.parse_args()
 
 
@@ -231,7 +232,7 @@ def main():
         opt.step()
         return losses[0]
 
-    use_graph = args.graph == "on"
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
     step = eager_step
     if use_graph:
         from vae2.graph import StepGraph
