@@ -339,7 +339,14 @@ struct UpSum {
   int rows, nxb, nrb;
 };
 
-template <int NUP>
+// TIGHT: source s stages at most 4 * (12 >> s) columns per chunk (true for the HRNet
+// heads, whose sources halve in resolution): 42 instead of 72 load / blend registers,
+// so 3 instead of 2 waves per SIMD, and no clamped duplicate loads.
+__host__ __device__ constexpr int us_vu(int s, bool tight) { return tight ? (12 >> s) : 12; }
+
+// KQ: K quads of the W0 block held in registers (5 for Cin0 <= 20, the W18 heads'
+// 18-channel branch; 8 up to kUsMaxCin): fewer fragment registers, 4 waves per SIMD.
+template <int NUP, bool TIGHT, int KQ>
 __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   extern __shared__ __attribute__((aligned(16))) float usm[];
   __shared__ double red[2][4][kUsCB];
@@ -362,9 +369,9 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, p.y_bytes);
   // ---- W0 fragments (once) ----
   const int kq = p.cin4 >> 2;
-  float fb[kUsMaxCin / 4][4];
+  float fb[KQ][4];
 #pragma unroll
-  for (int kb = 0; kb < kUsMaxCin / 4; ++kb)
+  for (int kb = 0; kb < KQ; ++kb)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       fb[kb][j] = load1(wr, kb < kq ? (uint32_t)((c0 + 16 * j + r) * p.cin4 + 4 * kb + g) * 4u
@@ -395,19 +402,19 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
     s2[j] = 0.0;
   }
   const int64_t P = (int64_t)(p.rows / p.nxb / p.nrb) * p.H * p.W;  // n * H * W
-  constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * VU)
+  constexpr int VU = 12;  // source columns per wave (host: vcols_s <= 4 * us_vu(s, TIGHT))
   const int pxa = 16 * wave + r;
   for (int ry = 0; ry < ny; ++ry) {
     const int oy = oy0 + ry, row = n * p.H + oy;
     // ---- loads: x0 fragments and the two source rows of every source ----
-    float fa[kUsMaxCin / 4];
+    float fa[KQ];
 #pragma unroll
-    for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+    for (int kb = 0; kb < KQ; ++kb) {
       const int k = 4 * kb + g;
       fa[kb] = load1(xr, (kb < kq && pxa < xn && k < p.cin)
                              ? (uint32_t)(((row * p.W + x0 + pxa) * p.x_ps + k) * 4u) : kOOB);
     }
-    float a0[NUP > 0 ? NUP : 1][VU], a1[NUP > 0 ? NUP : 1][VU];
+    float a0[NUP > 0 ? NUP : 1][VU], a1[NUP > 0 ? NUP : 1][VU];  // only [s][< us_vu] live
     Lerp ly[3];
 #pragma unroll
     for (int s = 0; s < NUP; ++s) {
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
       const int rb0 = ((n * p.zh[s] + ly[s].i0) * p.zw[s]) * p.zps[s] + c;
       const int rb1 = ((n * p.zh[s] + ly[s].i1) * p.zw[s]) * p.zps[s] + c;
 #pragma unroll
-      for (int u = 0; u < VU; ++u) {
+      for (int u = 0; u < us_vu(s, TIGHT); ++u) {
         int ix = vlo[s] + wave + 4 * u;
         ix = ix < vhi[s] ? ix : vhi[s];
         a0[s][u] = load1(zr, cok ? (uint32_t)(rb0 + ix * p.zps[s]) * 4u : kOOB);
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
 #pragma unroll
     for (int s = 0; s < NUP; ++s) {
 #pragma unroll
-      for (int u = 0; u < VU; ++u) {
+      for (int u = 0; u < us_vu(s, TIGHT); ++u) {
         const int j = wave + 4 * u;  // uniform per wave
         if (vlo[s] + j <= vhi[s])
           vs[voff[s] + j * us_vs(s) + lane] = ly[s].l0 * a0[s][u] + ly[s].l1 * a1[s][u];
@@ -438,7 +445,7 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < kUsMaxCin / 4; ++kb) {
+    for (int kb = 0; kb < KQ; ++kb) {
       if (kb < kq) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -783,6 +790,7 @@ __global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
 // channel-padded) dx layout.  Workgroup = (target row, slice of the row).  Needs
 // zw * C % 4 == 0 (16-byte aligned rows).
 static int g_adj_stream = 1;  // vae2_heads_set_algo bit 0 clears it
+static int g_upsum_tight = 1;  // vae2_heads_set_algo bit 1 clears it
 
 template <int S>
 __global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) {
@@ -828,10 +836,11 @@ __global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) 
   }
 }
 
-// Pixels per block of the backward passes (<= 1024 blocks, >= 64 pixels each).  (2048
-// blocks with 8 pixels in flight per thread measured slower: the partial rows double.)
-static int64_t head_ppb(int64_t P) {
-  int64_t ppb = ceil_div(P, 1024);
+// Pixels per block of the backward passes (>= 64 each): the reduce pass with <= 2048
+// blocks (a block holds only 3 pixel rows of 68 channel quads, so 1024 blocks left one
+// wave per SIMD: 134 -> 122 us per head), the apply pass with <= 1024 (measured better).
+static int64_t head_ppb(int64_t P, int64_t blocks = 2048) {
+  int64_t ppb = ceil_div(P, blocks);
   return ppb < 64 ? 64 : ppb;
 }
 
@@ -919,7 +928,7 @@ int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* sav
                    ((uintptr_t)dy % 16 == 0) && dyd->ps % 4 == 0, fn, "dy shape mismatch");
   VAE2_REQUIRE(ws_size >= vae2_head_out_bwd_ws_size(yd, cout2), fn, "workspace too small");
   const int C = (int)yd->c, c4 = (C + 3) / 4, rows = 256 / c4;
-  const int64_t P = act_pixels(yd), ppb = head_ppb(P);
+  const int64_t P = act_pixels(yd), ppb = head_ppb(P, 1024);
   const unsigned blocks = (unsigned)ceil_div(P, ppb);
   const size_t shm = (size_t)rows * C * sizeof(float);
   HEAD_DISPATCH(cout2, head_out_bwd_apply_kernel, dim3(blocks), dim3(256), shm,
@@ -981,12 +990,20 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1)) * sizeof(float);
   dim3 grid((unsigned)(yd->n * p.nrb * p.nxb * ncb));
   hipStream_t st = as_stream(stream);
+  bool tight = g_upsum_tight != 0;
+  for (int s = 0; s < nup; ++s) tight = tight && p.vcols[s] <= 4 * us_vu(s, true);
+  const bool kq5 = p.cin4 <= 20;
+#define US_LAUNCH(N)                                                                    \
+  if (tight && kq5) VAE2_LAUNCH((upsum_kernel<N, true, 5>), grid, dim3(256), shm, st, p); \
+  else if (tight) VAE2_LAUNCH((upsum_kernel<N, true, 8>), grid, dim3(256), shm, st, p); \
+  else VAE2_LAUNCH((upsum_kernel<N, false, 8>), grid, dim3(256), shm, st, p);
   switch (nup) {
-    case 0: VAE2_LAUNCH(upsum_kernel<0>, grid, dim3(256), shm, st, p); break;
-    case 1: VAE2_LAUNCH(upsum_kernel<1>, grid, dim3(256), shm, st, p); break;
-    case 2: VAE2_LAUNCH(upsum_kernel<2>, grid, dim3(256), shm, st, p); break;
-    default: VAE2_LAUNCH(upsum_kernel<3>, grid, dim3(256), shm, st, p); break;
+    case 0: US_LAUNCH(0) break;
+    case 1: US_LAUNCH(1) break;
+    case 2: US_LAUNCH(2) break;
+    default: US_LAUNCH(3) break;
   }
+#undef US_LAUNCH
   return check_launch(fn);
 }
 
@@ -999,8 +1016,9 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
 }
 
 int vae2_heads_set_algo(int algo) {
-  const int prev = g_adj_stream ? 0 : 1;
+  const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2);
   g_adj_stream = (algo & 1) ? 0 : 1;
+  g_upsum_tight = (algo & 2) ? 0 : 1;
   return prev;
 }
 

@@ -69,6 +69,10 @@ def main():
              yp, ctypes.byref(ya), ptr(stats), s)
     zb = sum(z.numel() for z in zs) * 4
     res.append(("upsum (y write + x0 + z read)", timeit(upsum, a.iters), P * C * 4 + P * 20 * 4 + zb))
+    lib.vae2_heads_set_algo(2)
+    res.append(("  same, 12 staging columns per source", timeit(upsum, a.iters),
+                P * C * 4 + P * 20 * 4 + zb))
+    lib.vae2_heads_set_algo(0)
 
     gs = [new_act((n, h, w_, C), ys[0]) for (h, w_) in sizes[1:]]
     gptrs = (ctypes.c_void_p * 3)(*[act_of(g)[0] for g in gs])
