@@ -609,16 +609,31 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
   if (tid < L.rows * c4) {
     const f4 mean = chan4(L.save, c, C), invstd = chan4(L.save + C, c, C);
     const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
-    for (int64_t p = p0 + r; p < p1; p += L.rows) {
-      const f4 xa = ld4(L.x + p * L.x_ps + c);
-      f4 ga = ld4(L.dy + p * L.dy_ps + c);
-      f4 ya;
-      if (y) ya = ld4(y + p * L.a_ps + c);
+    // kApplyU pixels' loads in flight per thread, then their math in pixel order (the
+    // same accumulation order as one pixel at a time)
+    for (int64_t pb = p0 + r; pb < p1; pb += (int64_t)kApplyU * L.rows) {
+      f4 xv[kApplyU], gv[kApplyU], yv[kApplyU];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (L.relu && !((y ? ya[k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f)) ga[k] = 0.f;
-        s0[k] += ga[k];
-        s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+      for (int u = 0; u < kApplyU; ++u) {
+        const int64_t p = pb + u * L.rows;
+        if (p < p1) {
+          xv[u] = ld4(L.x + p * L.x_ps + c);
+          gv[u] = ld4(L.dy + p * L.dy_ps + c);
+          if (y) yv[u] = ld4(y + p * L.a_ps + c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kApplyU; ++u) {
+        if (pb + u * L.rows >= p1) break;
+        const f4 xa = xv[u];
+        f4 ga = gv[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (L.relu && !((y ? yv[u][k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f))
+            ga[k] = 0.f;
+          s0[k] += ga[k];
+          s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+        }
       }
     }
 #pragma unroll
