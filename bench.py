@@ -78,6 +78,8 @@ def parse():
                          "tolerance line, BASELINE configs 2 and 5)")
     ap.add_argument("--conv-grouping", choices=("on", "off"), default="off",
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
+    ap.add_argument("--bn-apply-iters", type=int, default=None,
+                    help="pixels per thread / 4 of the BatchNorm apply kernels (A/B)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto: at N=1).  The "
                          "eager step measured 0-3%% faster on an idle host but 10-20%% "
@@ -198,6 +200,9 @@ def main():
     from vae2.optim import FusedAdam
     config = load_config(args)
     vdist.set_sync_bn(config.MI355X.SYNC_BN)
+    if args.bn_apply_iters is not None:
+        from vae2 import _lib
+        _lib.load().vae2_bn_set_apply_iters(args.bn_apply_iters)
     if args.conv_grouping == "on":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_grouping(1)

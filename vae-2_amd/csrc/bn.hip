@@ -551,7 +551,10 @@ struct BnLayer {
 struct BnMulti {
   BnLayer L[kBnMaxLayers];
   int n;
+  int iters;  // apply kernels: kApplyU * iters pixels per thread (vae2_bn_set_apply_iters)
 };
+
+static int g_bn_apply_iters = 1;
 
 __device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
   int i = 0;
@@ -559,13 +562,14 @@ __device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
   return i;
 }
 
-__device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
+__device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk, int iters) {
   const int C = L.C, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
   if (tid >= L.rows * c4) return;
   const int r = tid / c4, c = 4 * (tid - r * c4);
   const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
-  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  for (int it = 0; it < iters; ++it) {
+  const int64_t pb = ((int64_t)blk * iters + it) * L.rows * kApplyU + r;
   f4 v[kApplyU], rv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
@@ -588,11 +592,12 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
   }
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_apply_multi_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
-  bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
+  bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0, m.iters);
 }
 
 // Backward partials (sum g, sum g*xhat) of one layer's pixel range blk*ppb ...
@@ -662,7 +667,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_multi_kernel(BnMulti m) {
   bn_bwd_reduce_body(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
 }
 
-__device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
+__device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk, int iters) {
   const int C = L.C, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
   if (tid >= L.rows * c4) return;
@@ -682,7 +687,8 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
     mgx[k] = (float)L.sums[C + ch] * inv_n;
     k4[k] = (L.gamma ? L.gamma[ch] : 1.f) * invstd[k];
   }
-  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  for (int it = 0; it < iters; ++it) {
+  const int64_t pb = ((int64_t)blk * iters + it) * L.rows * kApplyU + r;
   f4 gv[kApplyU], xv[kApplyU], yv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
@@ -707,11 +713,12 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
     if (L.dres) st4(L.dres + p * L.dres_ps + c, g, c, C);
     st4(L.o + p * L.o_ps + c, o, c, C);
   }
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
-  bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
+  bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0, m.iters);
 }
 
 // One block per (layer, channel): reduce the layer's partial rows in double (fixed
@@ -818,6 +825,13 @@ int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
 using namespace vae2;
 
 extern "C" {
+
+int vae2_bn_set_apply_iters(int iters) {
+  const int prev = g_bn_apply_iters;
+  if (iters >= 1 && iters <= 8) g_bn_apply_iters = iters;
+  return prev;
+}
+
 
 int64_t vae2_bn_partial_rows(const vae2_act* xd) {
   int64_t P = act_pixels(xd);
@@ -1085,9 +1099,10 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
         L.ppb = pix_per_block(L.P);
         blocks += (int)ceil_div(L.P, L.ppb);
       } else {
-        blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU);
+        blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU * g_bn_apply_iters);
       }
     }
+    m.iters = kind == 1 ? 1 : g_bn_apply_iters;
     if (blocks == 0) continue;
     hipStream_t st = as_stream(stream);
     if (kind == 0)
