@@ -80,6 +80,8 @@ def parse():
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
     ap.add_argument("--bn-apply-iters", type=int, default=None,
                     help="pixels per thread / 4 of the BatchNorm apply kernels (A/B)")
+    ap.add_argument("--side-streams", choices=("on", "off"), default="on",
+                    help="posterior net / past decoder on side HIP streams (A/B)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto: at N=1).  The "
                          "eager step measured 0-3%% faster on an idle host but 10-20%% "
@@ -200,6 +202,9 @@ def main():
     from vae2.optim import FusedAdam
     config = load_config(args)
     vdist.set_sync_bn(config.MI355X.SYNC_BN)
+    if args.side_streams == "off":
+        from vae2 import streams as vstreams
+        vstreams.ENABLED = False
     if args.bn_apply_iters is not None:
         from vae2 import _lib
         _lib.load().vae2_bn_set_apply_iters(args.bn_apply_iters)
