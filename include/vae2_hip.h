@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 7
+#define VAE2_ABI_VERSION 8
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -271,6 +271,8 @@ typedef struct vae2_bn_layer {
   const double* countp;           /* device element count per channel (SyncBN: summed  */
   double count;                   /* over ranks), or NULL to use `count`               */
   int relu;
+  int dres_acc;                   /* backward apply: 1 = dres += masked dy (the residual  */
+                                  /* gradient summed onto another consumer's, in-kernel) */
 } vae2_bn_layer;
 /* y = relu?(fma(x, scale, shift) + a) per layer (vae2_bn_apply).                 */
 int vae2_bn_multi_apply(int n, const vae2_bn_layer* layers, void* stream);

@@ -546,6 +546,7 @@ struct BnLayer {
   double count;
   int64_t P, ppb;
   int C, x_ps, a_ps, o_ps, dy_ps, dres_ps, relu, rows, blk0;
+  int dres_acc;         // backward apply: dres += g instead of dres = g
 };
 
 struct BnMulti {
@@ -710,7 +711,10 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk, int
       const float xh = (xv[u][k] - mean[k]) * invstd[k];
       o[k] = k4[k] * (g[k] - mg[k] - xh * mgx[k]);
     }
-    if (L.dres) st4(L.dres + p * L.dres_ps + c, g, c, C);
+    if (L.dres) {
+      float* dr = L.dres + p * L.dres_ps + c;
+      st4(dr, L.dres_acc ? g + ld4(dr) : g, c, C);
+    }
     st4(L.o + p * L.o_ps + c, o, c, C);
   }
   }
@@ -1092,6 +1096,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       L.C = (int)l.xd.c;
       L.x_ps = (int)l.xd.ps; L.a_ps = (int)l.ad.ps; L.o_ps = (int)l.od.ps;
       L.dy_ps = (int)l.dyd.ps; L.dres_ps = (int)l.dresd.ps;
+      L.dres_acc = l.dres_acc;
       L.relu = l.relu;
       L.rows = quad_rows(l.xd.c);
       L.blk0 = blocks;

@@ -33,7 +33,7 @@ class BnLayer(ctypes.Structure):
     _fields_ = [("x", c_vp), ("xd", Act), ("a", c_vp), ("ad", Act), ("o", c_vp), ("od", Act),
                 ("dy", c_vp), ("dyd", Act), ("dres", c_vp), ("dresd", Act),
                 ("save", c_vp), ("gamma", c_vp), ("partials", c_vp), ("sums", c_vp),
-                ("countp", c_vp), ("count", c_f64), ("relu", c_int)]
+                ("countp", c_vp), ("count", c_f64), ("relu", c_int), ("dres_acc", c_int)]
 
 
 class BnFin(ctypes.Structure):
@@ -156,7 +156,7 @@ _SIGS = {
     "vae2_bn_set_apply_iters": (c_int, [c_int]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lib = None
 
 

@@ -288,7 +288,17 @@ def run_transition(trans, ys, nbranches):
     xs = [ys[i] if trans[i] is None else None for i in range(nbranches)]
     todo = [i for i in range(nbranches) if trans[i] is not None]
     firsts = [trans[i] if i < len(ys) else trans[i][0] for i in todo]
-    outs = _run_convbn_seqs(firsts, [ys[i] if i < len(ys) else ys[-1] for i in todo])
+    ins = [ys[i] if i < len(ys) else ys[-1] for i in todo]
+    # an input feeding two of these convs (the last branch: its own transition and the new
+    # branch's) gets one GradLink: the second data gradient accumulates in-kernel
+    links = [None] * len(ins)
+    for j in range(len(ins)):
+        users = [k for k in range(len(ins)) if ins[k] is ins[j]]
+        if len(users) > 1 and links[j] is None:
+            lk = ops.GradLink(len(users))
+            for k in users:
+                links[k] = lk
+    outs = _run_convbn_seqs(firsts, ins, x_links=links if any(links) else None)
     for i, x in zip(todo, outs):
         if i >= len(ys):
             for unit in list(trans[i])[1:]:

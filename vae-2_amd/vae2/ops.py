@@ -662,14 +662,21 @@ class _ConvBNMulti(torch.autograd.Function):
             rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
             part = _empty((2 * rows * cs[i],), r)
             dr = new_act(tuple(r.shape), r)
-            dres = new_act(tuple(r.shape), r) if ctx.has_res[i] and need[1 + 6 * i + 5] else None
+            dres, acc = None, 0
+            if ctx.has_res[i] and need[1 + 6 * i + 5]:
+                link = spec.res_link
+                if (link is not None and link.buf is not None and
+                        tuple(link.buf.shape) == tuple(r.shape) and _bn_quad_ok(link.buf)):
+                    dres, acc = link.buf, 1  # summed onto the other consumer's gradient in-kernel
+                else:
+                    dres = new_act(tuple(r.shape), r)
             gamma, beta = ctx.params[i][2], ctx.params[i][3]
             gsink, gret = _grad_sink(gamma, need[1 + 6 * i + 3])
             bsink, bret = _grad_sink(beta, need[1 + 6 * i + 4])
             sums_p = buf.data_ptr() + 8 * off
             countp = buf.data_ptr() + 8 * (tot + i) if group is not None else None
             lay[i] = _bn_layer(r, y if ctx.has_res[i] else None, dr, dy, dres, save, gamma,
-                               part, sums_p, countp, ctx.counts[i], spec.relu)
+                               part, sums_p, countp, ctx.counts[i], spec.relu, acc)
             fins[i] = _lib.BnFin(part.data_ptr(), rows, cs[i], sums_p, None, ctx.counts[i],
                                  None, None, None, None, None, 0.0, 0.0, None, _p(gsink),
                                  _p(bsink))
@@ -700,7 +707,7 @@ class _ConvBNMulti(torch.autograd.Function):
                 if dres is not None and link is not None:
                     if link.buf is None:
                         link.buf = dres
-                    else:
+                    elif link.buf is not dres:  # (dres is link.buf: summed in the BN kernel)
                         if cg.pending(link.buf):
                             cg.flush()
                         link.buf.add_(dres)
@@ -725,11 +732,12 @@ def _aligned_copy(t):
     return out
 
 
-def _bn_layer(x, a, o, dy, dres, save, gamma, part, sums_p, countp, count, relu):
+def _bn_layer(x, a, o, dy, dres, save, gamma, part, sums_p, countp, count, relu, dres_acc=0):
     def d(t):
         return act_of(t)[1] if t is not None else Act(0, 0, 0, 0, 0)
     return _lib.BnLayer(_p(x), d(x), _p(a), d(a), _p(o), d(o), _p(dy), d(dy), _p(dres), d(dres),
-                        _p(save), _p(gamma), _p(part), sums_p, countp, float(count), int(relu))
+                        _p(save), _p(gamma), _p(part), sums_p, countp, float(count), int(relu),
+                        int(dres_acc))
 
 
 BN_BATCH = True  # False: conv_bn_multi runs its layers one by one (A/B and parity tests)
