@@ -7,6 +7,7 @@ from helpers import GOLDEN
 from oracle.clips_ref import write_sequence_zip
 
 MODES = {1: "RGBA", 2: "L"}
+GOLDEN_DIR = GOLDEN
 
 
 def lib_dataset_class():

@@ -113,3 +113,15 @@ def test_incomplete_cache_is_rejected(tmp_path):
     json.dump(d, open(idx, "w"))
     with pytest.raises(RuntimeError, match="incomplete"):
         clips.ClipCache(cdir)
+
+
+def test_metrics_oracle_matches_reference_psnr():
+    """oracle/metrics_ref.py's to_image + PSNR / recon against the reference's own PSNR
+    (tests/golden/metrics.npz)."""
+    from clip_fixtures import GOLDEN_DIR
+    from oracle import metrics_ref
+    g = np.load(os.path.join(GOLDEN_DIR, "metrics.npz"))
+    for k in range(3):
+        ia, ib = metrics_ref.to_image(g[f"{k}/a"]), metrics_ref.to_image(g[f"{k}/b"])
+        assert abs(metrics_ref.psnr(ia, ib) - float(g[f"{k}/psnr"])) <= 1e-5 * abs(float(g[f"{k}/psnr"]))
+        assert abs(metrics_ref.recon_loss(ia, ib) - float(g[f"{k}/recon"])) <= 1e-5 * float(g[f"{k}/recon"])

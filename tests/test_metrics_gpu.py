@@ -99,3 +99,24 @@ def test_recon_psnr_and_frame_metrics():
         assert np.isnan(res[f, 2])  # 40x48 is below pytorch_msssim's MS-SSIM size bound
     psnr = float(metrics.PSNR()(ai[0], bi[0]))
     assert abs(psnr - res[0, 3]) < 1e-4
+
+
+def test_psnr_and_recon_match_reference_fixture():
+    """recon_loss and PSNR of the GPU metric path against the reference's own PSNR class
+    (tests/golden/metrics.npz, made by tests/golden/make_golden_metrics.py)."""
+    import os
+    from helpers import GOLDEN
+    from vae2 import metrics
+    g = np.load(os.path.join(GOLDEN, "metrics.npz"))
+    for k in range(3):
+        a = metrics.to_image(torch.from_numpy(g[f"{k}/a"])[None].cuda())
+        b = metrics.to_image(torch.from_numpy(g[f"{k}/b"])[None].cuda())
+        psnr = float(metrics.PSNR()(a, b))
+        s = metrics.absdiff_sqdiff(a, b).cpu()
+        recon = float(s[0]) / a.numel()
+        assert abs(psnr - float(g[f"{k}/psnr"])) <= 1e-5 * abs(float(g[f"{k}/psnr"]))
+        assert abs(recon - float(g[f"{k}/recon"])) <= 1e-5 * abs(float(g[f"{k}/recon"]))
+        if min(a.shape[-2:]) >= 11:  # the SSIM kernels need the 11-tap window to fit
+            res, _, _ = metrics.frame_metrics(torch.from_numpy(g[f"{k}/a"]).cuda(),
+                                              torch.from_numpy(g[f"{k}/b"]).cuda())
+            assert abs(res[0, 3] - float(g[f"{k}/psnr"])) <= 1e-5 * abs(float(g[f"{k}/psnr"]))
