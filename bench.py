@@ -78,8 +78,6 @@ def parse():
                          "tolerance line, BASELINE configs 2 and 5)")
     ap.add_argument("--conv-grouping", choices=("on", "off"), default="off",
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
-    ap.add_argument("--bn-apply-iters", type=int, default=None,
-                    help="pixels per thread / 4 of the BatchNorm apply kernels (A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
@@ -205,9 +203,6 @@ def main():
     if args.side_streams == "off":
         from vae2 import streams as vstreams
         vstreams.ENABLED = False
-    if args.bn_apply_iters is not None:
-        from vae2 import _lib
-        _lib.load().vae2_bn_set_apply_iters(args.bn_apply_iters)
     if args.conv_grouping == "on":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_grouping(1)

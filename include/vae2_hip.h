@@ -365,11 +365,6 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
 int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
                        float* y, const vae2_act* yd, void* stream);
 
-/* Pixels per thread of the multi-layer BatchNorm apply kernels (forward apply and
- * backward apply): 4 * iters (1..8; default 1).  Returns the previous setting.
- * Process-wide; tuning / A-B measurement.                                          */
-int vae2_bn_set_apply_iters(int iters);
-
 /* Head-kernel variants (A/B measurement): bit 0 = the per-channel-lane vertical pass of
  * the power-of-two upsampling adjoint instead of the row-streaming one; bit 1 = the
  * up-sum kernel with 12 staging columns for every source (instead of 12 / 6 / 3 for

@@ -552,10 +552,7 @@ struct BnLayer {
 struct BnMulti {
   BnLayer L[kBnMaxLayers];
   int n;
-  int iters;  // apply kernels: kApplyU * iters pixels per thread (vae2_bn_set_apply_iters)
 };
-
-static int g_bn_apply_iters = 1;
 
 __device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
   int i = 0;
@@ -563,14 +560,13 @@ __device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
   return i;
 }
 
-__device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk, int iters) {
+__device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
   const int C = L.C, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
   if (tid >= L.rows * c4) return;
   const int r = tid / c4, c = 4 * (tid - r * c4);
   const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
-  for (int it = 0; it < iters; ++it) {
-  const int64_t pb = ((int64_t)blk * iters + it) * L.rows * kApplyU + r;
+  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
   f4 v[kApplyU], rv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
@@ -593,12 +589,11 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk, int ite
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
   }
-  }
 }
 
 __global__ __launch_bounds__(256) void bn_apply_multi_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
-  bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0, m.iters);
+  bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
 }
 
 // Backward partials (sum g, sum g*xhat) of one layer's pixel range blk*ppb ...
@@ -668,7 +663,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_multi_kernel(BnMulti m) {
   bn_bwd_reduce_body(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
 }
 
-__device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk, int iters) {
+__device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   const int C = L.C, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
   if (tid >= L.rows * c4) return;
@@ -688,8 +683,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk, int
     mgx[k] = (float)L.sums[C + ch] * inv_n;
     k4[k] = (L.gamma ? L.gamma[ch] : 1.f) * invstd[k];
   }
-  for (int it = 0; it < iters; ++it) {
-  const int64_t pb = ((int64_t)blk * iters + it) * L.rows * kApplyU + r;
+  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
   f4 gv[kApplyU], xv[kApplyU], yv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
@@ -717,12 +711,11 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk, int
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
   }
-  }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
-  bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0, m.iters);
+  bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
 }
 
 // One block per (layer, channel): reduce the layer's partial rows in double (fixed
@@ -829,13 +822,6 @@ int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
 using namespace vae2;
 
 extern "C" {
-
-int vae2_bn_set_apply_iters(int iters) {
-  const int prev = g_bn_apply_iters;
-  if (iters >= 1 && iters <= 8) g_bn_apply_iters = iters;
-  return prev;
-}
-
 
 int64_t vae2_bn_partial_rows(const vae2_act* xd) {
   int64_t P = act_pixels(xd);
@@ -1104,10 +1090,9 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
         L.ppb = pix_per_block(L.P);
         blocks += (int)ceil_div(L.P, L.ppb);
       } else {
-        blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU * g_bn_apply_iters);
+        blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU);
       }
     }
-    m.iters = kind == 1 ? 1 : g_bn_apply_iters;
     if (blocks == 0) continue;
     hipStream_t st = as_stream(stream);
     if (kind == 0)

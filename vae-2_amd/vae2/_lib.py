@@ -153,7 +153,6 @@ _SIGS = {
     "vae2_heads_set_algo": (c_int, [c_int]),
     "vae2_conv2d_multi": (c_int, [c_int, c_vp, c_vp]),
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
-    "vae2_bn_set_apply_iters": (c_int, [c_int]),
 }
 
 ABI_VERSION = 8
