@@ -1,3 +1,5 @@
+# Diagnostic: which ATen add kernels (autograd gradient accumulation) remain in one
+# bench-geometry training step, with their shapes.   gpurun -- python scripts/_find_adds.py
 import sys, os, collections
 sys.path.insert(0, 'vae-2_amd'); sys.path.insert(0, 'tests'); sys.path.insert(0, '.')
 import torch

@@ -62,15 +62,29 @@ __global__ __launch_bounds__(256) void head_out_fwd_kernel(
     float acc[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) acc[o] = 0.f;
-    for (int q = l; q < c4; q += 16) {
-      const f4 v = hld4(yb_at(y, P, p, 4 * q));
-      const f4 a = ssc[q], b = ssh[q];
+    // up to kHeadQU quads per lane with their loads in flight together (the same
+    // quad order as one at a time)
+    constexpr int kHeadQU = 5;
+    for (int q0 = l; q0 < c4; q0 += 16 * kHeadQU) {
+      f4 vv[kHeadQU];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float h = __builtin_fmaf(v[k], a[k], b[k]);
-        h = (4 * q + k < C && !(h < 0.f)) ? h : 0.f;  // NaN propagates
+      for (int u = 0; u < kHeadQU; ++u) {
+        const int q = q0 + 16 * u;
+        vv[u] = q < c4 ? hld4(yb_at(y, P, p, 4 * q)) : f4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
-        for (int o = 0; o < CO; ++o) acc[o] += h * sw[o * c4 + q][k];
+      for (int u = 0; u < kHeadQU; ++u) {
+        const int q = q0 + 16 * u;
+        if (q >= c4) break;
+        const f4 v = vv[u];
+        const f4 a = ssc[q], b = ssh[q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float h = __builtin_fmaf(v[k], a[k], b[k]);
+          h = (4 * q + k < C && !(h < 0.f)) ? h : 0.f;  // NaN propagates
+#pragma unroll
+          for (int o = 0; o < CO; ++o) acc[o] += h * sw[o * c4 + q][k];
+        }
       }
     }
 #pragma unroll
