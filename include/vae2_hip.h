@@ -434,6 +434,19 @@ int vae2_global_avgpool_fwd(const float* x, const vae2_act* xd, float* y,
                             void* stream);
 int vae2_global_avgpool_bwd(const float* dy, const vae2_act* dyd, float* dx,
                             const vae2_act* dxd, float beta, void* stream);
+/* AdaptiveAvgPool2d((1,1)) of F.upsample(x, (H, W), bilinear) (enc_hrnet.py:1022-1025,
+ * the posterior net's pooled concat) without the full-resolution tensor: the mean of a
+ * bilinear upsampling is a separably weighted sum at the source resolution,
+ * y[n][c] = scale * sum_{iy,ix} x[n][iy][ix][c] * wr[iy] * wc[ix]  (wr / wc: device
+ * [h] / [w] column sums of the interpolation weights, scale = 1 / (H*W)); ws:
+ * vae2_spatial_ws_size(xd) floats.  The backward is the weighted broadcast
+ * dx (+)= scale * dy[n][c] * wr[iy] * wc[ix]  (beta 0: overwrite, 1: accumulate).       */
+int vae2_weighted_avgpool_fwd(const float* x, const vae2_act* xd, const float* wr,
+                              const float* wc, float scale, float* y, const vae2_act* yd,
+                              float* ws, int64_t ws_size, void* stream);
+int vae2_weighted_avgpool_bwd(const float* dy, const vae2_act* dyd, const float* wr,
+                              const float* wc, float scale, float* dx, const vae2_act* dxd,
+                              float beta, void* stream);
 
 /* ------------------------------------------------------------- ELBO ---- */
 

@@ -667,3 +667,34 @@ def test_conv2d_multi_grouped_equals_single_calls():
     for ta, tb in zip(a, b):
         for u, v in zip(ta, tb):
             assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("hw", [(32, 64), (30, 22), (128, 256)])
+def test_up_avgpool_equals_upsample_then_pool(hw):
+    """ops.up_avgpool (weighted pooling at the branch resolutions: vae2_weighted_avgpool_*)
+    against avgpool(up_cat(xs)) (the materialised full-resolution concatenation), forward
+    and backward."""
+    from vae2 import ops
+    torch.manual_seed(2)
+    H, W = hw
+    sizes = [(H, W)]
+    for _ in range(3):
+        sizes.append(((sizes[-1][0] + 1) // 2, (sizes[-1][1] + 1) // 2))
+    like = torch.empty(1, device=DEV)
+    xs = [ops.new_act((2, h, w, c), like).normal_() for (h, w), c in zip(sizes, (18, 36, 72, 144))]
+    g = torch.randn(2, 1, 1, 270, device=DEV)
+    outs = []
+    for fused in (True, False):
+        ops.UP_AVGPOOL = fused
+        try:
+            leaves = [x.detach().clone().requires_grad_() for x in xs]
+            y = ops.up_avgpool(leaves)
+            y.backward(g)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), [t.grad for t in leaves]))
+        finally:
+            ops.UP_AVGPOOL = True
+    (y1, g1), (y0, g0) = outs
+    assert rel(y1, y0) < 1e-6
+    for a, b in zip(g1, g0):
+        assert rel(a, b) < 1e-6

@@ -383,17 +383,27 @@ __global__ __launch_bounds__(256) void copy_act_kernel(const float* __restrict__
 }
 
 // y[n,h,w,c] = scale * v[n*vs + c] + beta * y
+// y[n, iy, ix, c] (+)= scale * v[n][c] (* wr[iy] * wc[ix] when wr != null: the adjoint of
+// a separably weighted spatial sum)
 __global__ __launch_bounds__(256) void tile_kernel(const float* __restrict__ v, int64_t vs,
                                                    float* __restrict__ y, Act yd, float scale,
-                                                   float beta, FastDiv cdiv, FastDiv hwdiv) {
+                                                   float beta, FastDiv cdiv, FastDiv hwdiv,
+                                                   const float* __restrict__ wr = nullptr,
+                                                   const float* __restrict__ wc = nullptr,
+                                                   FastDiv wdiv = FastDiv()) {
   const uint32_t C = (uint32_t)yd.c;
   const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * C;
+  const uint32_t HW = (uint32_t)(yd.h * yd.w);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += gridDim.x * blockDim.x) {
     uint32_t p = cdiv.div(i);
     uint32_t c = i - p * C;
     uint32_t n = hwdiv.div(p);
     float val = scale * v[(int64_t)n * vs + c];
+    if (wr) {
+      const uint32_t q = p - n * HW, iy = wdiv.div(q);
+      val *= wr[iy] * wc[q - iy * (uint32_t)yd.w];
+    }
     float* dst = y + (int64_t)p * yd.ps + c;
     *dst = (beta != 0.f) ? val + beta * *dst : val;
   }
@@ -402,7 +412,9 @@ __global__ __launch_bounds__(256) void tile_kernel(const float* __restrict__ v, 
 // Spatial sums per (n, c): stage 1 partials over pixel chunks.
 __global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __restrict__ x,
                                                                Act xd, int64_t ppb,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part,
+                                                               const float* __restrict__ wr = nullptr,
+                                                               const float* __restrict__ wc = nullptr) {
   __shared__ float red[256];
   const int C = (int)xd.c;
   const int64_t HW = xd.h * xd.w;
@@ -418,7 +430,12 @@ __global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __re
     float s = 0.f;
     if (tid < S) {
       const int c = tid % C, rr = tid / C;
-      for (int64_t p = p0 + rr; p < p1; p += R) s += base[p * xd.ps + c];
+      if (wr) {
+        for (int64_t p = p0 + rr; p < p1; p += R)
+          s += base[p * xd.ps + c] * (wr[p / xd.w] * wc[p % xd.w]);
+      } else {
+        for (int64_t p = p0 + rr; p < p1; p += R) s += base[p * xd.ps + c];
+      }
     }
     red[tid] = s;
     __syncthreads();
@@ -430,7 +447,8 @@ __global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __re
   } else {
     for (int c = tid; c < C; c += 256) {
       float s = 0.f;
-      for (int64_t p = p0; p < p1; ++p) s += base[p * xd.ps + c];
+      for (int64_t p = p0; p < p1; ++p)
+        s += base[p * xd.ps + c] * (wr ? wr[p / xd.w] * wc[p % xd.w] : 1.f);
       out[c] = s;
     }
   }
@@ -461,12 +479,13 @@ static int64_t spatial_chunks(const vae2_act* xd, int64_t* ppb_out) {
 
 static int spatial_sum(const float* x, const vae2_act* xd, float* out, int64_t os,
                        float scale, int accumulate, float* part, int64_t ws_size,
-                       hipStream_t s, const char* fn) {
+                       hipStream_t s, const char* fn, const float* wr = nullptr,
+                       const float* wc = nullptr) {
   int64_t ppb = 0;
   int64_t chunks = spatial_chunks(xd, &ppb);
   VAE2_REQUIRE(part && ws_size >= xd->n * chunks * xd->c, fn, "workspace too small");
   VAE2_LAUNCH(spatial_partials_kernel, dim3((unsigned)chunks, (unsigned)xd->n),
-                     dim3(256), 0, s, x, to_act(xd), ppb, part);
+                     dim3(256), 0, s, x, to_act(xd), ppb, part, wr, wc);
   int rc = check_launch(fn);
   if (rc) return rc;
   int64_t nc = xd->n * xd->c;
@@ -762,6 +781,30 @@ int vae2_global_avgpool_fwd(const float* x, const vae2_act* xd, float* y,
                "output must be (n, 1, 1, c)");
   return spatial_sum(x, xd, y, yd->ps, 1.f / (float)(xd->h * xd->w), 0, ws, ws_size,
                      as_stream(stream), fn);
+}
+
+int vae2_weighted_avgpool_fwd(const float* x, const vae2_act* xd, const float* wr,
+                              const float* wc, float scale, float* y, const vae2_act* yd,
+                              float* ws, int64_t ws_size, void* stream) {
+  const char* fn = "vae2_weighted_avgpool_fwd";
+  VAE2_REQUIRE(x && y && wr && wc && act_ok(xd) && act_ok(yd), fn, "bad arguments");
+  VAE2_REQUIRE(yd->h == 1 && yd->w == 1 && yd->n == xd->n && yd->c == xd->c, fn,
+               "output must be (n, 1, 1, c)");
+  return spatial_sum(x, xd, y, yd->ps, scale, 0, ws, ws_size, as_stream(stream), fn, wr, wc);
+}
+
+int vae2_weighted_avgpool_bwd(const float* dy, const vae2_act* dyd, const float* wr,
+                              const float* wc, float scale, float* dx, const vae2_act* dxd,
+                              float beta, void* stream) {
+  const char* fn = "vae2_weighted_avgpool_bwd";
+  VAE2_REQUIRE(dy && dx && wr && wc && act_ok(dyd) && act_ok(dxd), fn, "bad arguments");
+  VAE2_REQUIRE(dyd->h == 1 && dyd->w == 1 && dyd->n == dxd->n && dyd->c == dxd->c, fn,
+               "dy must be (n, 1, 1, c)");
+  int64_t total = act_elems(dxd);
+  VAE2_LAUNCH(tile_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream), dy,
+              dyd->ps, dx, to_act(dxd), scale, beta, FastDiv((uint32_t)dxd->c),
+              FastDiv((uint32_t)(dxd->h * dxd->w)), wr, wc, FastDiv((uint32_t)dxd->w));
+  return check_launch(fn);
 }
 
 int vae2_global_avgpool_bwd(const float* dy, const vae2_act* dyd, float* dx,

@@ -152,6 +152,10 @@ _SIGS = {
     "vae2_avgpool2x2": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "vae2_heads_set_algo": (c_int, [c_int]),
     "vae2_conv2d_multi": (c_int, [c_int, c_vp, c_vp]),
+    "vae2_weighted_avgpool_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_f32, c_vp, P_ACT, c_vp,
+                                          c_i64, c_vp]),
+    "vae2_weighted_avgpool_bwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_f32, c_vp, P_ACT, c_f32,
+                                          c_vp]),
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 

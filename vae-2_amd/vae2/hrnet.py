@@ -604,7 +604,7 @@ class HighResolutionNetEDz(HighResolutionNet):
                                      "(the reference fails here too)")
                 out.append(ops.conv(y, m[0]))
             return out
-        h = ops.avgpool(ops.up_cat(ys))
+        h = ops.up_avgpool(ys)  # avgpool(cat(y0, up(y1), ...)): enc_hrnet.py:1022-1025
         h = ops.conv_bn(h, self.last_layer[1], self.last_layer[2], relu=True)
         return ops.conv(h, self.last_layer[4])
 

@@ -1028,6 +1028,108 @@ def avgpool(x):
     return _AvgPool.apply(x)
 
 
+_POOLW = {}
+
+
+def _pool_weights(n_in, n_out, device):
+    """Sum over the n_out outputs of each input's bilinear weight (align_corners=False,
+    F.upsample's index rule in fp32: src = max(0, (o + 0.5) * n_in / n_out - 0.5))."""
+    key = (n_in, n_out, str(device))
+    t = _POOLW.get(key)
+    if t is None:
+        import numpy as np
+        w = np.zeros(n_in, dtype=np.float64)
+        scale = np.float32(n_in) / np.float32(n_out)
+        for o in range(n_out):
+            src = max(np.float32(0.0), np.float32(scale * np.float32(o + 0.5) - np.float32(0.5)))
+            i0 = int(src)
+            l1 = float(src - np.float32(i0))
+            i1 = i0 + 1 if i0 < n_in - 1 else i0
+            w[i0] += 1.0 - l1
+            w[i1] += l1
+        t = torch.tensor(w, dtype=torch.float32, device=device)
+        _POOLW[key] = t
+    return t
+
+
+class _UpAvgPool(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) of cat([x0, up(x1), up(x2), ...]) at x0's resolution
+    (enc_hrnet.py:1022-1025): the upsampled branches are pooled at their own resolution
+    with the bilinear weights' column sums, so the full-resolution concatenation (and its
+    gradient) is never materialised."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        x0 = xs[0]
+        n, H, W, _ = x0.shape
+        ctot = sum(t.shape[3] for t in xs)
+        y = _empty((n, 1, 1, ctot), x0)
+        s = stream_ptr()
+        scale = 1.0 / (H * W)
+        off = 0
+        ws_keep = []
+        for t in xs:
+            c = t.shape[3]
+            tp, ta = act_of(t)
+            ya = Act(n, 1, 1, c, ctot)
+            yp = ctypes.c_void_p(y.data_ptr() + 4 * off)
+            wsz = _lib.load().vae2_spatial_ws_size(ctypes.byref(ta))
+            ws = _empty((max(wsz, 1),), x0)
+            ws_keep.append(ws)
+            if t.shape[1:3] == x0.shape[1:3]:
+                call("vae2_global_avgpool_fwd", tp, ctypes.byref(ta), yp, ctypes.byref(ya),
+                     ptr(ws), wsz, s)
+            else:
+                wr = _pool_weights(t.shape[1], H, x0.device)
+                wc = _pool_weights(t.shape[2], W, x0.device)
+                call("vae2_weighted_avgpool_fwd", tp, ctypes.byref(ta), ptr(wr), ptr(wc),
+                     scale, yp, ctypes.byref(ya), ptr(ws), wsz, s)
+            off += c
+        ctx.shapes = [tuple(t.shape) for t in xs]
+        ctx.hw = (H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        H, W = ctx.hw
+        s = stream_ptr()
+        ctot = dy.shape[3]
+        grads = []
+        off = 0
+        for i, shp in enumerate(ctx.shapes):
+            c = shp[3]
+            if not ctx.needs_input_grad[i]:
+                grads.append(None)
+                off += c
+                continue
+            dx = new_act(shp, dy)
+            dxp, dxa = act_of(dx)
+            da = Act(shp[0], 1, 1, c, ctot)
+            dp_ = ctypes.c_void_p(dy.data_ptr() + 4 * off)
+            if shp[1:3] == (H, W):
+                call("vae2_global_avgpool_bwd", dp_, ctypes.byref(da), dxp, ctypes.byref(dxa),
+                     0.0, s)
+            else:
+                wr = _pool_weights(shp[1], H, dy.device)
+                wc = _pool_weights(shp[2], W, dy.device)
+                call("vae2_weighted_avgpool_bwd", dp_, ctypes.byref(da), ptr(wr), ptr(wc),
+                     1.0 / (H * W), dxp, ctypes.byref(dxa), 0.0, s)
+            grads.append(dx)
+            off += c
+        return tuple(grads)
+
+
+UP_AVGPOOL = True  # False: materialise up_cat(xs) then avgpool (A/B and parity tests)
+
+
+def up_avgpool(xs):
+    """avgpool(up_cat(xs)) without the full-resolution concatenation."""
+    if not UP_AVGPOOL:
+        return avgpool(up_cat(xs))
+    return _UpAvgPool.apply(*xs)
+
+
 # ---------------------------------------------------------------- layout ----
 class _ToNHWC(torch.autograd.Function):
     @staticmethod
