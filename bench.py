@@ -132,6 +132,22 @@ def pmc_traffic(kernel):
     return best
 
 
+def head_skip_gflop_per_clip(ed, H, W):
+    """FLOPs the reference spends on its 270-channel heads that the commuted per-branch
+    head path (vae2/heads.py) does not: per head and per direction (forward, data grad,
+    weight grad) the full-resolution C x C 1x1 conv, 2*C*C*H*W, against the branch products
+    at branch resolution, 2*C*sum_b(c_b*H_b*W_b); 3 heads in each of the encoder and the two
+    decoders (enc_hrnet.py:833-847)."""
+    split = [int(c) for c in ed.last_stage_channels]
+    C = sum(split)
+    sizes = [(H, W)]
+    for _ in split[1:]:
+        h, w = sizes[-1]
+        sizes.append(((h + 1) // 2, (w + 1) // 2))
+    branch = sum(c * h * w for c, (h, w) in zip(split, sizes))
+    return 3 * 3 * 3 * 2.0 * C * (C * H * W - branch) / 1e9  # nets x heads x directions
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -313,6 +329,19 @@ def main():
             roof["traffic_unit"] = "HBM bytes/launch (PMC, profiles/)"
             roof["step_frac"] = round(conv_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["step_gflop"] = round(conv_gf, 1)
+            if ref_gf is not None and L == 3:
+                # the noted conv + head FLOPs must equal the reference's FlopCounter total
+                # less what the commuted heads legitimately skip (tests assert "reconciled")
+                skip = B * head_skip_gflop_per_clip(ed, H, W)
+                want = B * ref_gf - skip
+                roof["flop_reconciliation"] = {
+                    "noted_gflop_per_step": round(conv_gf, 1),
+                    "reference_gflop_per_step": round(B * ref_gf, 1),
+                    "commuted_head_skip_gflop_per_step": round(skip, 1),
+                    "expected_gflop_per_step": round(want, 1),
+                    "ratio": round(conv_gf / want, 4),
+                    "reconciled": abs(conv_gf / want - 1.0) < 0.01,
+                    "note_conflicts": summ["note_conflicts"]}
             if ref_gf is not None and L == 3:
                 roof["step_frac_ref_flops"] = round(
                     B * ref_gf / ms / prof.MFMA_PEAK_TF, 4)

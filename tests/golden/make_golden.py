@@ -7,7 +7,7 @@ lib/core/criterion.py) read-only, with the two shims SURVEY.md App. C lists
 only (inputs, noise, outputs, loss terms, gradients, checksums) as .npz here.
 Nothing from the reference is copied.
 
-    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz (+ the .pth.tar)
 
 Cases
   tiny_native   tiny HRNet, 32x32, B=2, L=3, Z=4, VAE_NATIVE:
@@ -27,6 +27,17 @@ Cases
                 G step with the LSGAN terms through both discriminators (utils.py:114-119),
                 Adam, then the D step (FullModel_D, utils.py:256-276) and its Adam;
                 G and D gradients, D losses, running statistics, parameter sums
+  tiny_vaegan   IS_BASELINE + VAE_GAN: L1(x2t_hat, x3t) + KL + both LSGAN terms on x2t_hat
+                (utils.py:132-141), decoders under no_grad; the D step takes x3t as the real
+                sample (function.py:503-504)
+  tiny_eval     evaluation forward (function.py:60,124-136): model_encdec.eval() (BatchNorm
+                on running statistics, discriminators included), sampling_mode
+                'prior_sampling', no_grad, on a trained-looking state (Kaiming-scale conv
+                weights, random BN affine and running statistics, stored as sd/<key>)
+  ref_ckpt      a checkpoint the reference itself writes (train.py:320-324 format:
+                epoch / state_dict / optimizer_encdec, torch.save) after one Adam step,
+                -> ref_checkpoint_encdec.pth.tar; ref_ckpt.npz holds the next training
+                step taken from that state (noise, loss terms, parameter sums after Adam)
 
     python tests/golden/make_golden.py [case ...]   # default: all cases
 """
@@ -181,7 +192,9 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
         for key, sd in (("ds", init_ds), ("df", init_df)):
             _, s3, a3 = checksums(sd)
             out[f"init_{key}_sum"], out[f"init_{key}_abs"] = torch.as_tensor(s3), torch.as_tensor(a3)
-        run_d_step(out, fm, ds, df, params, xt, x2t, x2p, lsgan_adversarial_loss, FullModel_D)
+        # the D step's real sample: x2t, or x3t in baseline mode (function.py:503-504)
+        real = x3t if baseline else x2t
+        run_d_step(out, fm, ds, df, params, xt, real, x2p, lsgan_adversarial_loss, FullModel_D)
     if adam_steps:
         ps = [p for n, p in list(ez.named_parameters()) + list(ed.named_parameters())]
         opt = torch.optim.Adam([{"params": ps}], lr=1e-4)
@@ -207,9 +220,10 @@ def run_case(tag, tiny, hd=False, baseline=False, mode="VAE_NATIVE", B=2, H=32, 
     print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
 
 
-def run_d_step(out, fm, ds, df, gparams, xt, x2t, x2p, lsgan, FullModel_D):
+def run_d_step(out, fm, ds, df, gparams, xt, real, x2p, lsgan, FullModel_D):
     """The rest of one adversarial_train iteration (function.py:499-512): Adam on the
-    generator (encz + ED, 'D_model' excluded, train.py:251-256), then the D step."""
+    generator (encz + ED, 'D_model' excluded, train.py:251-256), then the D step with
+    `real` as the real sample."""
     import torch
     opt_g = torch.optim.Adam([{"params": [p for _, p in gparams]}], lr=1e-4)
     opt_g.step()
@@ -217,7 +231,7 @@ def run_d_step(out, fm, ds, df, gparams, xt, x2t, x2p, lsgan, FullModel_D):
     fmd.train()
     dparams = list(ds.named_parameters(prefix="ds")) + list(df.named_parameters(prefix="df"))
     opt_d = torch.optim.Adam([{"params": [p for _, p in dparams]}], lr=1e-4)
-    dl = fmd(x2t=x2t, x2t_predict=x2p.detach())
+    dl = fmd(x2t=real, x2t_predict=x2p.detach())
     for n, v in zip(("D_all", "D_seq", "D_frame"), dl):
         out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]))
     opt_d.zero_grad()
@@ -250,7 +264,120 @@ CASES = {
     "tiny_det": dict(tiny=True, baseline=True, mode="DETERMINISTIC", full_grads=True),
     "tiny_prior": dict(tiny=True, sampling="prior_sampling", full_grads=True),
     "tiny_gan": dict(tiny=True, gan=1.0, full_grads=True),
+    "tiny_vaegan": dict(tiny=True, baseline=True, mode="VAE_GAN", gan=1.0, full_grads=True),
 }
+
+
+def _full_model(gan):
+    """Tiny ED / EDz / D-seq / D-frame in train.py:79-82 order and FullModel_encdec."""
+    import torch
+    import models.enc_hrnet as eh
+    from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
+    from utils.utils import FullModel_encdec
+    cfg = make_cfg(True)
+    torch.manual_seed(0)
+    ed = eh.get_encdec_model(cfg)
+    ez = eh.get_encz_model(cfg)
+    ds = eh.get_D_sequence_model(cfg)
+    df = eh.get_D_frame_model(cfg)
+    fm = FullModel_encdec(ez, ed, ds, df, L1Loss(), KLLoss(), lsgan_adversarial_loss(),
+                          1.0, 0.1, 1.0, gan)
+    return fm, cfg
+
+
+def _inputs(B=2, H=32, W=32, L=3):
+    import torch
+    g = torch.Generator().manual_seed(1)
+    return [torch.randn(B, 3 * L, H, W, generator=g) for _ in range(3)]
+
+
+def run_eval(tag="tiny_eval", B=2):
+    """Eval-mode prior-sampling forward (function.py:60,124-136) on a trained-looking state."""
+    import torch
+    fm, cfg = _full_model(gan=1.0)
+    zc = cfg.MODEL.EXTRA.Z_DIM
+    gen = torch.Generator().manual_seed(7)
+    sd = fm.state_dict()
+    with torch.no_grad():
+        for k in sorted(sd):
+            v = sd[k]
+            if not v.is_floating_point():
+                continue
+            stem = k.rsplit(".", 1)[0]
+            is_bn = stem + ".running_mean" in sd
+            if k.endswith("running_mean"):
+                v.copy_(0.3 * torch.randn(v.shape, generator=gen))
+            elif k.endswith("running_var"):
+                v.copy_(0.5 + 1.5 * torch.rand(v.shape, generator=gen))
+            elif v.dim() == 4:  # conv weight: variance-preserving scale
+                v.copy_(torch.randn(v.shape, generator=gen) / float(v[0].numel()) ** 0.5)
+            elif k.endswith(".weight") and is_bn:
+                v.copy_(1.0 + 0.2 * torch.randn(v.shape, generator=gen))
+            else:  # BN bias, conv bias
+                v.copy_(0.1 * torch.randn(v.shape, generator=gen))
+    fm.eval()
+    xt, x2t, x3t = _inputs(B)
+    torch.manual_seed(321)
+    with torch.no_grad():
+        losses, x1p, x2p, x3p = fm(xt, x2t, x3t, 1.0, sampling_mode="prior_sampling")
+    torch.manual_seed(321)  # replay: z (prior) then the encoder's random code
+    z = torch.randn(B, zc, 1, 1)
+    code = torch.randn(B, zc, 1, 1)
+    out = {"xt": xt, "x2t": x2t, "x3t": x3t, "eps": z, "code": code,
+           "x1p": x1p, "x2p": x2p, "x3p": x3p}
+    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL", "gan_seq", "gan_frame"]
+    for n, v in zip(names, losses):
+        out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]) if torch.is_tensor(v) else v)
+    for k, v in fm.state_dict().items():
+        out["sd/" + k] = v
+    arrays = {k: v.detach().numpy() for k, v in out.items()}
+    path = os.path.join(HERE, f"{tag}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def run_ckpt(tag="ref_ckpt", B=2):
+    """The reference's own checkpoint (train.py:320-324) after one ELBO step + Adam, and
+    the next step taken from it."""
+    import torch
+    fm, cfg = _full_model(gan=0.0)
+    zc = cfg.MODEL.EXTRA.Z_DIM
+    fm.train()
+    named = [(n, p) for n, p in fm.named_parameters() if p.requires_grad and "D_model" not in n]
+    opt = torch.optim.Adam([{"params": [p for _, p in named]}], lr=1e-4)  # train.py:251-256
+    xt, x2t, x3t = _inputs(B)
+    torch.manual_seed(123)
+    losses = fm(xt, x2t, x3t, 1.0)[0]
+    opt.zero_grad()
+    losses[0].backward()
+    opt.step()
+    ck = os.path.join(HERE, "ref_checkpoint_encdec.pth.tar")
+    torch.save({"epoch": 1, "state_dict": fm.state_dict(),
+                "optimizer_encdec": opt.state_dict()}, ck)
+    print(f"wrote {ck} ({os.path.getsize(ck) / 1e6:.2f} MB)")
+    torch.manual_seed(124)
+    losses = fm(xt, x2t, x3t, 1.0)[0]
+    torch.manual_seed(124)
+    eps = torch.randn(B, zc, 1, 1)
+    code = torch.randn(B, zc, 1, 1)
+    out = {"xt": xt, "x2t": x2t, "x3t": x3t, "eps": eps, "code": code}
+    names = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
+    for n, v in zip(names, losses):
+        out["loss_" + n] = torch.as_tensor(float(v.reshape(-1)[0]))
+    opt.zero_grad()
+    losses[0].backward()
+    opt.step()
+    pn, psum, pabs = checksums({n: p.detach() for n, p in named})
+    out["param_sum"] = torch.as_tensor(psum)
+    out["param_abs"] = torch.as_tensor(pabs)
+    arrays = {k: v.detach().numpy() for k, v in out.items()}
+    arrays["param_names"] = np.array(pn)
+    path = os.path.join(HERE, f"{tag}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+EXTRA = {"tiny_eval": run_eval, "ref_ckpt": run_ckpt}
 
 
 def main():
@@ -259,8 +386,11 @@ def main():
     np.int = int  # the reference uses the removed numpy alias (enc_hrnet.py:321,596,700)
     import torch
     torch.set_num_threads(8)
-    for tag in (sys.argv[1:] or list(CASES)):
-        run_case(tag, **CASES[tag])
+    for tag in (sys.argv[1:] or list(CASES) + list(EXTRA)):
+        if tag in EXTRA:
+            EXTRA[tag]()
+        else:
+            run_case(tag, **CASES[tag])
 
 
 if __name__ == "__main__":

@@ -58,6 +58,24 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 
 
+def load_eval_state(g, nets):
+    """tiny_eval.npz's trained-looking FullModel_encdec state (sd/<key>) into the modules
+    (ez, ed, ds, df) (parameters are copied in place: flat-buffer views stay valid)."""
+    prefixes = ("encz_model.", "encdec_model.", "D_model_sequence.", "D_model_frame.")
+    for pre, m in zip(prefixes, nets):
+        dev = next(m.parameters()).device
+        sd = {k[3 + len(pre):]: torch.from_numpy(np.asarray(g[k])).to(dev)
+              for k in g.files if k.startswith("sd/" + pre)}
+        m.load_state_dict(sd, strict=True)
+
+
+def ref_checkpoint():
+    """The checkpoint the reference itself wrote (make_golden.py ref_ckpt), loaded with a
+    loader that executes nothing from the file."""
+    return torch.load(os.path.join(GOLDEN, "ref_checkpoint_encdec.pth.tar"), map_location="cpu",
+                      weights_only=True)
+
+
 def t(a):
     return torch.from_numpy(np.asarray(a))
 

@@ -29,11 +29,17 @@ B = 4
 NAMES = ["loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"]
 
 
-def _inputs():
-    gen = torch.Generator().manual_seed(11)
-    xs = [torch.randn(B, 6, 64, 64, generator=gen) for _ in range(3)]
-    eps = torch.randn(B, 10, 1, 1, generator=gen)
-    code = torch.randn(B, 10, 1, 1, generator=gen)
+# BASELINE config 5: 256x512 (the reference's default IMAGE_SIZE), "10-frame" -> L=3 (9
+# frames), bf16, B=2 (the bench's --height 256 --width 512 --batch 2 line)
+KW5 = dict(arch="w18", hw=(256, 512), L=3, classes=3)
+B5 = 2
+
+
+def _inputs(b=B, L=2, hw=(64, 64), seed=11):
+    gen = torch.Generator().manual_seed(seed)
+    xs = [torch.randn(b, 3 * L, *hw, generator=gen) for _ in range(3)]
+    eps = torch.randn(b, 10, 1, 1, generator=gen)
+    code = torch.randn(b, 10, 1, 1, generator=gen)
     return xs, eps, code
 
 
@@ -42,13 +48,13 @@ def _set_bf16(on):
     return _lib.load().vae2_conv2d_set_mfma_bf16(1 if on else 0)
 
 
-def _run(bf16, xs, eps, code, steps=0, lr=1e-3):
+def _run(bf16, xs, eps, code, steps=0, lr=1e-3, kw=KW):
     """HIP forward (+ `steps` Adam steps on the same batch): losses per step, x2t_hat."""
     from vae2.optim import FusedAdam
     prev = _set_bf16(bf16)
     try:
         torch.manual_seed(0)
-        fm = hip_model(KW)
+        fm = hip_model(kw)
         opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=lr)
         xd = [x.to(DEV) for x in xs]
         hist, x2 = [], None
@@ -91,6 +97,41 @@ def test_bf16_config2_training_tracks_fp32():
     xs = [0.1 * x for x in xs]
     h32, _ = _run(False, xs, eps, code, steps=6, lr=3e-3)
     h16, _ = _run(True, xs, eps, code, steps=6, lr=3e-3)
+    assert abs(h16[0][0] - h32[0][0]) <= 2e-3 * h32[0][0]
+    for i, (a, b) in enumerate(zip(h16, h32)):
+        assert abs(a[0] - b[0]) <= 0.15 * abs(b[0]), (i, a[0], b[0])
+
+
+def test_bf16_config5_forward_against_fp32_oracle():
+    """Config 5 geometry (256x512, L=3, B=2): the bf16-operand forward against the fp32
+    CPU oracle with the bf16 tolerances (loss terms 1e-2, x2t_hat rel-L2 1e-1); the fp32
+    operand path at the fp32 bounds (1e-5 / 1e-4)."""
+    from oracle import ref_cpu
+    xs, eps, code = _inputs(B5, 3, (256, 512), seed=13)
+    torch.manual_seed(0)
+    ed, ez = build(make_cfg(**KW5))
+    with torch.no_grad():
+        terms, preds, _ = ref_cpu.elbo(ez, ed, *xs, eps, code)
+    ref = [float(terms[n]) for n in NAMES]
+    # bf16: x2t_hat rel-L2 1e-1 at this size (measured 5.4e-2: twice the pixels per BN
+    # channel of config 2 and the same ~100 bf16-rounded convs in front of the heads)
+    for bf16, tl, tx in ((False, 1e-5, 1e-4), (True, 1e-2, 1e-1)):
+        hist, x2p = _run(bf16, xs, eps, code, kw=KW5)
+        for n, a, b in zip(NAMES, hist[0], ref):
+            assert abs(a - b) <= tl * abs(b) + 1e-6, (bf16, n, a, b)
+        x2 = x2p.permute(0, 3, 1, 2) if x2p.shape[1] != preds[1].shape[1] else x2p
+        assert rel(x2, preds[1]) < tx, (bf16, rel(x2, preds[1]))
+
+
+def test_bf16_config5_training_tracks_fp32():
+    """Config 5 training step (256x512, B=2) with bf16 operands: 5 Adam steps (lr 1e-3; at
+    3e-3 the two trajectories part by 15 % at step 2 at this size) on one low-amplitude
+    batch track the fp32-operand run (first loss within 2e-3, every later one within 15 %)."""
+    xs, eps, code = _inputs(B5, 3, (256, 512), seed=14)
+    xs = [0.1 * x for x in xs]
+    h32, _ = _run(False, xs, eps, code, steps=5, lr=1e-3, kw=KW5)
+    h16, _ = _run(True, xs, eps, code, steps=5, lr=1e-3, kw=KW5)
+    print("loss fp32", [round(h[0], 1) for h in h32], "bf16", [round(h[0], 1) for h in h16])
     assert abs(h16[0][0] - h32[0][0]) <= 2e-3 * h32[0][0]
     for i, (a, b) in enumerate(zip(h16, h32)):
         assert abs(a[0] - b[0]) <= 0.15 * abs(b[0]), (i, a[0], b[0])

@@ -118,6 +118,95 @@ def test_direct_conv3x3(shape):
         assert rel(cg.bias.grad, conv.bias.grad) < TOL
 
 
+REMAINDER_SHAPES = [
+    # N, H, W, Cin, Cout, bias: 18 / 36 / 72-channel outputs (forward) and inputs (data
+    # gradient) as 16*TN MFMA columns + NR VALU channels, 8-row (TM 4) and 4-row tiles
+    (8, 128, 256, 18, 18, False),  # TM 4, NR 2 both directions
+    (8, 64, 128, 36, 36, True),    # TM 2, NR 4 (two lanes per pixel)
+    (2, 32, 64, 72, 72, False),    # TM 2, NR 8
+    (4, 64, 96, 36, 18, False),    # forward NR 2, data gradient NR 4
+    (2, 13, 40, 18, 36, True),     # partial row / column tiles
+]
+
+
+@pytest.mark.parametrize("shape", REMAINDER_SHAPES)
+def test_direct_conv3x3_valu_remainder(shape):
+    """dconv3 with the VALU remainder (vae2_conv2d_set_algo bit 16 clear): forward, data
+    gradient, weight gradient and the BN-statistics epilogue against PyTorch, and the
+    remainder instances are the ones launched."""
+    from vae2 import _lib, ops
+    torch.manual_seed(5)
+    n, h, w, cin, cout, bias = shape
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias)
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    y_ref = conv(x)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    cg = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    lib = _lib.load()
+    prev = lib.vae2_conv2d_set_algo(2)
+    lib.vae2_kernel_log(1)
+    try:
+        xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+        with torch.no_grad():
+            xg.copy_(nhwc(x.detach()).to(DEV))
+        xg.requires_grad_(True)
+        lib.vae2_kernel_log_read(None, 0)
+        yg = ops.conv(xg, cg)
+        yg.backward(nhwc(gy).to(DEV))
+        torch.cuda.synchronize()
+        import ctypes
+        buf = ctypes.create_string_buffer(1 << 14)
+        lib.vae2_kernel_log_read(buf, len(buf))
+        names = buf.value.decode().split(";")
+        # BN statistics from the remainder epilogue (conv_bn: running mean / var)
+        bn, bg = nn.BatchNorm2d(cout, momentum=0.5), nn.BatchNorm2d(cout, momentum=0.5).to(DEV)
+        with torch.no_grad():
+            ops.conv_bn(xg.detach(), cg, bg, relu=False)
+            bn(conv(x.detach()))
+        torch.cuda.synchronize()
+    finally:
+        lib.vae2_kernel_log(0)
+        lib.vae2_conv2d_set_algo(prev)
+    for c in (cout, cin):
+        nr = c % 16
+        if nr in (2, 4, 8) and c // 16 in (1, 2, 4):
+            assert any(k.endswith(f", {nr}>") and k.startswith("dconv3_kernel") for k in names), \
+                (c, names)
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(nchw(xg.grad), x.grad) < TOL
+    assert rel(cg.weight.grad, conv.weight.grad) < TOL
+    if bias:
+        assert rel(cg.bias.grad, conv.bias.grad) < TOL
+    assert rel(bg.running_mean, bn.running_mean) < 1e-5
+    assert rel(bg.running_var, bn.running_var) < 1e-5
+
+
+@pytest.mark.parametrize("cout", [18, 36])
+def test_valu_remainder_equals_padded_tiles(cout):
+    """The remainder path (bit 16 clear) and the all-MFMA padded tiles (bit 16 set) compute
+    the same conv: equal up to fp32 summation order."""
+    from vae2 import _lib, ops
+    torch.manual_seed(8)
+    lib = _lib.load()
+    x = ops.new_act((8, 64, 128, 36), torch.empty(1, device=DEV))
+    x.normal_()
+    w = torch.randn(cout, 36, 3, 3, device=DEV) * 0.05
+    outs = []
+    prev = lib.vae2_conv2d_set_algo(2)
+    try:
+        for algo in (2, 2 + 16):
+            lib.vae2_conv2d_set_algo(algo)
+            conv = nn.Conv2d(36, cout, 3, 1, 1, bias=False).to(DEV)
+            with torch.no_grad():
+                conv.weight.copy_(w)
+                outs.append(ops.conv(x, conv).clone())
+    finally:
+        lib.vae2_conv2d_set_algo(prev)
+    assert rel(outs[0], outs[1]) < 1e-6
+
+
 BF16_SHAPES = [
     # N, H, W, Cin, Cout, k, stride, bias, algo: every conv kernel with bf16 operands
     (2, 16, 32, 18, 18, 3, 1, False, 2),    # direct 3x3 (dconv3 fwd / dgrad, wgrad3)
@@ -308,6 +397,49 @@ def test_conv_bn_train(relu, res, stride, cout):
     assert rel(bn_g.running_mean, bn_c.running_mean) < 1e-5
     assert rel(bn_g.running_var, bn_c.running_var) < 1e-5
     assert int(bn_g.num_batches_tracked) == int(bn_c.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_conv_bn_residual_link_accumulates(aligned):
+    """A residual whose GradLink buffer already holds the other consumer's gradient: the
+    BN backward apply sums its residual gradient onto that buffer in-kernel
+    (vae2_bn_layer.dres_acc: the multi-layer path, aligned residual) or with an add (the
+    per-layer path an unaligned residual view takes); either way the residual's gradient
+    is the reference's plus the prefilled contribution."""
+    from vae2 import ops
+    torch.manual_seed(2)
+    n, h, w, c = 2, 10, 12, 18
+    conv = nn.Conv2d(c, c, 3, 1, 1, bias=False)
+    bn = nn.BatchNorm2d(c, momentum=0.01)
+    nn.init.normal_(bn.weight, 1.0, 0.2)
+    x = torch.randn(n, c, h, w, requires_grad=True)
+    r = torch.randn(n, c, h, w, requires_grad=True)
+    y_ref = F.relu(bn(conv(x)) + r)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    other = torch.randn(n, h, w, c)
+    conv_g, bn_g = nn.Conv2d(c, c, 3, 1, 1, bias=False).to(DEV), nn.BatchNorm2d(c, momentum=0.01).to(DEV)
+    conv_g.load_state_dict(conv.state_dict())
+    bn_g.load_state_dict(bn.state_dict())
+    xg = ops.new_act((n, h, w, c), torch.empty(1, device=DEV))
+    rg = (ops.new_act((n, h, w, c), xg) if aligned
+          else torch.zeros(n, h, w, c + 3, device=DEV)[..., 1:1 + c])
+    assert ops._bn_quad_ok(rg) == aligned
+    with torch.no_grad():
+        xg.copy_(nhwc(x.detach()).to(DEV))
+        rg.copy_(nhwc(r.detach()).to(DEV))
+    rg.requires_grad_(True)
+    link = ops.GradLink(2)
+    link.buf = ops.new_act((n, h, w, c), xg)
+    with torch.no_grad():
+        link.buf.copy_(other.to(DEV))
+    link.done = 1  # the other consumer's backward ran first and handed the buffer on
+    yg = ops.conv_bn_multi([xg], [conv_g], [bn_g], True, residuals=[rg], res_links=[link])[0]
+    yg.backward(nhwc(gy).to(DEV))
+    torch.cuda.synchronize()
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(rg.grad.cpu(), nhwc(r.grad) + other) < 1e-5
+    assert rel(conv_g.weight.grad, conv.weight.grad) < 1e-4
 
 
 KS_SHAPES = [

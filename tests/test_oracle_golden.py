@@ -5,7 +5,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import build, checksums, golden, make_cfg, max_rel, rel, t
+from helpers import (build, checksums, golden, load_eval_state, make_cfg, max_rel, ref_checkpoint,
+                     rel, t)
 from oracle import ref_cpu
 
 CASES = {
@@ -191,3 +192,85 @@ def test_oracle_gan_iteration_matches_reference():
                                g["g_param_sum"], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(checksums({n: p.detach() for n, p in dparams})[0],
                                g["d_param_sum"], rtol=1e-4, atol=1e-6)
+
+
+def test_oracle_vaegan_baseline_matches_reference():
+    """IS_BASELINE + VAE_GAN (utils.py:132-141): L1(x2t_hat, x3t) + KL + both LSGAN terms,
+    decoders under no_grad; the D step's real sample is x3t (function.py:503-504)."""
+    torch.set_num_threads(8)
+    g = golden("tiny_vaegan")
+    ed, ez, ds, df = build(make_cfg("tiny", baseline=True, mode="VAE_GAN"), with_d=True)
+    xt, x2t, x3t = t(g["xt"]), t(g["x2t"]), t(g["x3t"])
+    terms, (x1p, x2p, x3p), _ = ref_cpu.elbo(ez, ed, xt, x2t, x3t, t(g["eps"]), t(g["code"]),
+                                             is_baseline=True, baseline_mode="VAE_GAN",
+                                             ds=ds, df=df, gan_lambda=1.0)
+    for name, v in terms.items():
+        ref = float(g["loss_" + name])
+        assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-7, (name, float(v), ref)
+    assert max_rel(x2p, t(g["x2p"])) < 1e-4
+    gparams = list(ez.named_parameters(prefix="encz")) + list(ed.named_parameters(prefix="ed"))
+    opt_g = torch.optim.Adam([p for _, p in gparams], lr=1e-4)
+    terms["loss_all"].backward()
+    _grad_check(gparams, g)
+    assert all(p.grad is None for n, p in gparams if n.startswith("ed.dec"))  # no_grad decoders
+    opt_g.step()
+    dparams = list(ds.named_parameters(prefix="ds")) + list(df.named_parameters(prefix="df"))
+    for p in (p for _, p in dparams):
+        p.grad = None
+    dl = ref_cpu.d_losses(ds, df, x3t, x2p)
+    for name, v in zip(("D_all", "D_seq", "D_frame"), dl):
+        ref = float(g["loss_" + name])
+        assert abs(float(v.reshape(-1)[0]) - ref) <= 1e-5 * abs(ref), (name, float(v), ref)
+    dl[0].backward()
+    _grad_check(dparams, g, "dgrad")
+
+
+def test_oracle_eval_prior_sampling_matches_reference():
+    """Evaluation forward (function.py:60,124-136): eval() BatchNorm on running statistics
+    (discriminators too), prior sampling, no_grad."""
+    torch.set_num_threads(8)
+    g = golden("tiny_eval")
+    ed, ez, ds, df = build(make_cfg("tiny"), with_d=True)
+    load_eval_state(g, (ez, ed, ds, df))
+    for m in (ed, ez, ds, df):
+        m.eval()
+    with torch.no_grad():
+        terms, (x1p, x2p, x3p), _ = ref_cpu.elbo(ez, ed, t(g["xt"]), t(g["x2t"]), t(g["x3t"]),
+                                                 t(g["eps"]), t(g["code"]), prior=True,
+                                                 ds=ds, df=df, gan_lambda=1.0)
+    for name, v in terms.items():
+        ref = float(g["loss_" + name])
+        assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-7, (name, float(v), ref)
+    for k, p in (("x1p", x1p), ("x2p", x2p), ("x3p", x3p)):
+        assert max_rel(p, t(g[k])) < 1e-5, k
+
+
+def test_reference_checkpoint_interchange():
+    """A checkpoint the reference itself wrote (train.py:320-324: epoch / state_dict /
+    optimizer_encdec) loads strictly into this package's FullModel_encdec tree, and the
+    oracle's next step from it (loss terms, torch Adam from the saved moments) is the
+    reference's (tests/golden/ref_ckpt.npz)."""
+    torch.set_num_threads(8)
+    from vae2.model import FullModel_encdec
+    ck = ref_checkpoint()
+    assert ck["epoch"] == 1 and set(ck) == {"epoch", "state_dict", "optimizer_encdec"}
+    ed, ez, ds, df = build(make_cfg("tiny"), with_d=True)
+    fm = FullModel_encdec(ez, ed, ds, df, None, None, None, 1.0, 0.1, 1.0, 0.0)
+    assert list(fm.state_dict()) == list(ck["state_dict"])
+    fm.load_state_dict(ck["state_dict"], strict=True)
+    g = golden("ref_ckpt")
+    named = [(n, p) for n, p in fm.named_parameters() if "D_model" not in n]
+    assert len(ck["optimizer_encdec"]["state"]) == len(named)
+    opt = torch.optim.Adam([{"params": [p for _, p in named]}], lr=1e-4)
+    opt.load_state_dict(ck["optimizer_encdec"])
+    terms, _, _ = ref_cpu.elbo(ez, ed, t(g["xt"]), t(g["x2t"]), t(g["x3t"]), t(g["eps"]),
+                               t(g["code"]))
+    for name in ("loss_all", "xt_recon", "x2t_recon", "x3t_recon", "z_KL"):
+        ref = float(g["loss_" + name])
+        assert abs(float(terms[name]) - ref) <= 1e-5 * abs(ref) + 1e-7, (name, ref)
+    opt.zero_grad()
+    terms["loss_all"].backward()
+    opt.step()
+    assert [n for n, _ in sorted(named)] == list(g["param_names"])
+    np.testing.assert_allclose(checksums({n: p.detach() for n, p in named})[0], g["param_sum"],
+                               rtol=1e-4, atol=1e-6)

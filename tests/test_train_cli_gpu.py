@@ -15,21 +15,21 @@ YAML = os.path.join(ROOT, "vae-2_amd", "experiments", "vae2_w18_small_v2_128x256
 pytestmark = pytest.mark.gpu
 
 
-def _train(tmp_path, *opts):
+def _train(tmp_path, *opts, cfg=YAML, size="[64, 32]"):
     if TOOLS not in sys.path:
         sys.path.insert(0, TOOLS)
     import train  # vae-2_amd/tools/train.py
     from config import config
     config.defrost()
-    config.merge_from_file(YAML)  # reset anything a previous run merged
+    config.merge_from_file(cfg)  # reset anything a previous run merged
     config.freeze()
-    argv = ["--cfg", YAML, "OUTPUT_DIR", str(tmp_path / "output"), "LOG_DIR", str(tmp_path / "log"),
-            "TRAIN.IMAGE_SIZE", "[64, 32]", "TRAIN.BATCH_SIZE_PER_GPU", "2",
+    argv = ["--cfg", cfg, "OUTPUT_DIR", str(tmp_path / "output"), "LOG_DIR", str(tmp_path / "log"),
+            "TRAIN.IMAGE_SIZE", size, "TRAIN.BATCH_SIZE_PER_GPU", "2",
             "MI355X.SYNTHETIC_CLIPS", "4", "PRINT_FREQ", "1", "MI355X.DEFER_CHECKS", "True",
             *opts]
     train.main(argv)
     return os.path.join(str(tmp_path / "output"), "cityscapessequence",
-                        os.path.basename(YAML).split(".")[0])
+                        os.path.basename(cfg).split(".")[0])
 
 
 def test_train_cli_elbo_checkpoint_and_resume(tmp_path):
@@ -123,3 +123,34 @@ def test_train_and_inference_cli_on_sequence_zips(tmp_path, cache):
         assert len(lines) == 2 and abs(float(lines[1]) - m[1, 0, 1]) < 1e-6
         pngs = [f for f in os.listdir(os.path.join(vis, f"{tag}predict")) if f.endswith(".png")]
         assert len(pngs) == 2 * 3
+
+
+def test_train_cli_resumes_a_reference_checkpoint(tmp_path):
+    """TRAIN.RESUME (train.py:270-290) from checkpoint_encdec.pth.tar as the reference
+    itself writes it (tests/golden/ref_checkpoint_encdec.pth.tar: the tiny HRNet after one
+    Adam step, discriminator keys included): the run continues at epoch 1 with the saved
+    Adam moments (step counter 1 + 2 iterations)."""
+    import shutil
+    import yaml
+    from helpers import _TINY, GOLDEN
+    with open(YAML) as f:
+        cfg = yaml.safe_load(f)
+    cfg["MODEL"]["EXTRA"].update({k: dict(v) for k, v in _TINY.items()})
+    cfg["MODEL"]["EXTRA"]["Z_DIM"] = 4
+    tiny = str(tmp_path / "vae2_tiny.yaml")
+    with open(tiny, "w") as f:
+        yaml.safe_dump(cfg, f)
+    out = tmp_path / "output" / "cityscapessequence" / "vae2_tiny"
+    out.mkdir(parents=True)
+    shutil.copy(os.path.join(GOLDEN, "ref_checkpoint_encdec.pth.tar"),
+                str(out / "checkpoint_encdec.pth.tar"))
+    ref = torch.load(str(out / "checkpoint_encdec.pth.tar"), map_location="cpu", weights_only=True)
+    _train(tmp_path, "TRAIN.END_EPOCH", "2", "TRAIN.RESUME", "True", "MI355X.ELBO_ONLY", "True",
+           cfg=tiny, size="[32, 32]")
+    ck = torch.load(str(out / "checkpoint_encdec.pth.tar"), map_location="cpu", weights_only=True)
+    assert ck["epoch"] == 2
+    assert int(float(ck["optimizer_encdec"]["state"][0]["step"])) == 3
+    assert set(ck["state_dict"]) == {k for k in ref["state_dict"] if not k.startswith("D_model")}
+    w0 = ref["state_dict"]["encdec_model.conv1.weight"]
+    w1 = ck["state_dict"]["encdec_model.conv1.weight"]
+    assert not torch.equal(w0, w1) and float((w1 - w0).abs().max()) < 1e-3  # 2 Adam steps

@@ -25,6 +25,12 @@
 
 #include "common.h"
 
+// Diagnostic builds only (never the shipped library): -DVAE2_ABLATE=1 stages zeros
+// instead of loading the direct kernel's halo tile, =2 drops its output stores.
+#ifndef VAE2_ABLATE
+#define VAE2_ABLATE 0
+#endif
+
 namespace vae2 {
 
 
@@ -390,12 +396,25 @@ constexpr int kDcMaxCs4 = 8;  // quads per slab
 
 // One output tile: bm = tile index (image-major), by = N block, nrows = tiles of the
 // layer (rows of its BN partial statistics).
-template <int TM, int TN, bool FLIP, bool BF>
+//
+// NR > 0 (fp32 operands, one N block): the layer's last NR output channels (N = 16*TN +
+// NR, NR in {2, 4, 8}: the 18 / 36 / 72-channel branches) are computed on the VALU
+// beside the MFMAs instead of in a further 16-wide MFMA tile that would be mostly
+// padding: lane = one output pixel of the wave's 16*TM (and, at TM = 2, one half of the
+// NR channels), v_fma_f32 chains over the same (tap, channel) K order the chunks walk,
+// with the remainder weights of the slab staged in LDS (broadcast reads).  The MFMA work
+// of an 18-channel layer halves (32 -> 16 columns), of a 36-channel one drops by 1/3.
+template <int TM, int TN, bool FLIP, bool BF, int NR = 0>
 __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const int by,
                                             const int nrows, float* __restrict__ tile) {
   constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
-  __shared__ float red[4][2][BN];
+  constexpr int BNT = BN + NR;             // channels of this block (MFMA + VALU)
+  constexpr int PPW = 16 * TM;             // output pixels per wave
+  constexpr int LPP = NR ? 64 / PPW : 1;   // lanes per pixel (remainder channel groups)
+  constexpr int NRL = NR / LPP;            // remainder channels per lane
+  static_assert(NR == 0 || (!BF && NR % LPP == 0 && NRL >= 1 && NRL <= 8), "remainder shape");
+  __shared__ float red[4][2][BNT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int per_img = p.tiles_h * p.tiles_w;
@@ -435,12 +454,31 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   };
+  // VALU remainder: this lane's pixel (same tile rows / columns as the MFMA A rows) and
+  // channel group; its accumulators; the slab's remainder weights rw[NR][9][cs4*4] in LDS
+  const int rl = lane % PPW, rh = lane / PPW;
+  const int rtrow = wave * (TM / 2) + ((rl >> 4) >> 1), rtcol = ((rl >> 4) & 1) * 16 + (rl & 15);
+  const int rbase = ((rtrow + 1) * LW + rtcol + 1) * csp;
+  float* const rw = tile + LH * LW * csp;
+  const int rws = 9 * p.cs4 * 4;  // floats per remainder channel in rw
+  float racc[NRL > 0 ? NRL : 1];
+#pragma unroll
+  for (int j = 0; j < NRL; ++j) racc[j] = 0.f;
 
   const int img_base = img * p.img_h;
   for (int q0 = 0; q0 < Q; q0 += p.cs4) {
     const int qs = Q - q0 < p.cs4 ? Q - q0 : p.cs4;
     // ---- stage the halo tile of this slab (zero outside the image / past a_c) ----
     __syncthreads();
+    if constexpr (NR > 0) {  // remainder weights of the slab, tap-major, FLIP applied
+      const int per = 9 * qs * 4;
+      for (int i = threadIdx.x; i < NR * per; i += 256) {
+        const int j = i / per, rem = i - j * per;
+        const int t = rem / (qs * 4), c = rem - t * (qs * 4);
+        const int tl = FLIP ? 8 - t : t;
+        rw[j * rws + t * (qs * 4) + c] = p.w[(int64_t)(BN + j) * kk4 + tl * p.a_c4 + q0 * 4 + c];
+      }
+    }
     // thread -> (channel quad q = tid % qs, pixels pb, pb + pstride, ...); SB loads in
     // flight per thread before their LDS stores (few round trips, few extra registers)
     constexpr int SB = 3;
@@ -458,6 +496,8 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
           const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
           const bool ok = pix < LH * LW && (unsigned)ih < (unsigned)p.img_h &&
                           (unsigned)iw < (unsigned)p.img_w;
+          if (VAE2_ABLATE & 1) v[u] = f4{(float)pix, (float)ih, (float)iw, (float)c};
+          else
           v[u] = load4(arsrc, ok ? (uint32_t)(((img_base + ih) * p.img_w + iw) * p.a_ps + c) * 4u
                                  : kOOB);
         }
@@ -495,13 +535,38 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       q += 4;
       while (q >= qs) { q -= qs; ++t; }
     };
+    // the remainder's share of chunk ch: its 4 (tap, quad) K steps (wave-uniform)
+    auto rem = [&](int ch) {
+      if constexpr (NR > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kq = ch * 4 + u;
+          if (kq < 9 * qs) {
+            const int t = kq / qs, q = kq - t * qs;
+            const int dh = (t >= 3) + (t >= 6) - 1, dw = t - 3 * (dh + 1) - 1;
+            const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + (dh * LW + dw) * csp + 4 * q]);
+#pragma unroll
+            for (int j = 0; j < NRL; ++j) {
+              const f4 wv = *reinterpret_cast<const f4*>(
+                  &rw[(rh * NRL + j) * rws + t * (qs * 4) + 4 * q]);
+              racc[j] = __builtin_fmaf(xv[0], wv[0], racc[j]);
+              racc[j] = __builtin_fmaf(xv[1], wv[1], racc[j]);
+              racc[j] = __builtin_fmaf(xv[2], wv[2], racc[j]);
+              racc[j] = __builtin_fmaf(xv[3], wv[3], racc[j]);
+            }
+          }
+        }
+      }
+    };
     if (!BF) {
       load(fa0, fb0);
       for (int ch = 0; ch < nch; ch += 2) {
         load(fa1, fb1);
         mma(fa0, fb0);
+        rem(ch);
         load(fa0, fb0);
         mma(fa1, fb1);
+        rem(ch + 1);
       }
     } else {  // bf16 operands: one 16x16x32 MFMA per chunk pair
       load(fa0, fb0);
@@ -542,10 +607,27 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         float v = acc[i][j][e];
         if (p.bias) v += p.bias[n];
         if (p.beta != 0.f) v += p.beta * yrow[n];
-        yrow[n] = v;
+        if (!(VAE2_ABLATE & 2) || v == 1234.5f) yrow[n] = v;
         csum[j] += v;
         csq[j] += v * v;
       }
+    }
+  }
+  // the VALU remainder's outputs: NRL consecutive channels of this lane's pixel
+  float rsum[NRL > 0 ? NRL : 1], rsq[NRL > 0 ? NRL : 1];
+  if constexpr (NR > 0) {
+    const int oh = oh0 + rtrow, ow = ow0 + rtcol;
+    const bool in = oh < p.img_h && ow < p.img_w;
+    const int nb = BN + rh * NRL;
+    float* yrow = p.y + (int64_t)((img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0)) * p.y_ps + nb;
+#pragma unroll
+    for (int j = 0; j < NRL; ++j) {
+      float v = racc[j];
+      if (p.bias) v += p.bias[nb + j];
+      if (p.beta != 0.f && in) v += p.beta * yrow[j];
+      if (in && (!(VAE2_ABLATE & 2) || v == 1234.5f)) yrow[j] = v;
+      rsum[j] = in ? v : 0.f;
+      rsq[j] = in ? v * v : 0.f;
     }
   }
   if (p.stats) {
@@ -563,9 +645,26 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         red[wave][1][j * 16 + r] = csq[j];
       }
     }
+    if constexpr (NR > 0) {  // sum over the wave's pixels (lanes of one channel group)
+#pragma unroll
+      for (int j = 0; j < NRL; ++j) {
+#pragma unroll
+        for (int o = 1; o < PPW; o <<= 1) {
+          rsum[j] += __shfl_xor(rsum[j], o, 64);
+          rsq[j] += __shfl_xor(rsq[j], o, 64);
+        }
+      }
+      if (rl == 0) {
+#pragma unroll
+        for (int j = 0; j < NRL; ++j) {
+          red[wave][0][BN + rh * NRL + j] = rsum[j];
+          red[wave][1][BN + rh * NRL + j] = rsq[j];
+        }
+      }
+    }
     __syncthreads();
     const int rows = nrows;
-    for (int c = threadIdx.x; c < BN; c += 256) {
+    for (int c = threadIdx.x; c < BNT; c += 256) {
       if (n0 + c >= p.n) continue;
       float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
       float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
@@ -575,11 +674,11 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   }
 }
 
-template <int TM, int TN, bool FLIP, bool BF = false>
+template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0>
 __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  dconv3_body<TM, TN, FLIP, BF>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
-                                tile);
+  dconv3_body<TM, TN, FLIP, BF, NR>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
+                                    tile);
 }
 
 // Up to kDcGroup independent layers with the same tile shape in one launch (the lock-
@@ -1300,7 +1399,10 @@ static int g_conv_algo = 0;  // 0 auto, 1 gather kernel only, 2 direct wherever 
 
 struct DTile {
   int tm, tn, nblk, cs4, tiles_h, tiles_w;
+  int nr = 0;  // output channels on the VALU beside the MFMA tiles (dconv3_body NR)
 };
+
+static int g_dconv_nr = 0;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
 
 static bool dconv_legal(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
                         const float* a) {
@@ -1308,18 +1410,30 @@ static bool dconv_legal(const vae2_act* ad, const vae2_act* yd, int k, int strid
          vec_ok(a, (int)ad->ps);
 }
 
-static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd) {
+// remainder = true: an N of 16*TN + NR with (TN, NR) = (1, 2), (2, 4) or (4, 8) (the 18 /
+// 36 / 72-channel branches) takes TN MFMA tiles plus NR VALU channels in one N block
+// (fp32 operands only).
+static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder = true) {
   DTile d;
   Tile t = pick_tile(act_pixels(yd), (int)yd->c);
   d.tn = t.tn;
   d.nblk = t.nblk;
+  const int N = (int)yd->c, tn = N / 16, nr = N % 16;
+  if (remainder && g_dconv_nr && !g_bf16 &&
+      ((tn == 1 && nr == 2) || (tn == 2 && nr == 4) || (tn == 4 && nr == 8))) {
+    d.tn = tn;
+    d.nr = nr;
+    d.nblk = 1;
+  }
   const int Q = round_up((int)ad->c, 4) / 4;
   const int nsl = (Q + kDcMaxCs4 - 1) / kDcMaxCs4;
   d.cs4 = (Q + nsl - 1) / nsl;  // balanced slabs
   d.tiles_w = (int)ceil_div(yd->w, kDcBW);
   // 8-row tiles unless that leaves fewer than ~3 workgroups per CU
   d.tm = 4;
-  if (yd->h < 8 || ad->n * ceil_div(yd->h, 8) * d.tiles_w * d.nblk < 768) d.tm = 2;
+  // (from the all-MFMA N blocking, so the tile rows and the BN partial-statistics rows
+  //  do not depend on the remainder switch or the grouped path)
+  if (yd->h < 8 || ad->n * ceil_div(yd->h, 8) * d.tiles_w * t.nblk < 768) d.tm = 2;
   d.tiles_h = (int)ceil_div(yd->h, 2 * d.tm);
   return d;
 }
@@ -1330,12 +1444,19 @@ static bool dconv_use(const vae2_act* ad, const vae2_act* yd, int k, int stride,
   if (g_conv_algo == 2) return true;
   // auto: enough workgroups to fill the chip (narrow images waste partial 32-column
   // tiles and low-resolution layers have too few tiles: the gather kernel wins there)
-  DTile d = pick_dtile(ad, yd);
+  DTile d = pick_dtile(ad, yd, false);
   return ad->w >= 16 && ad->n * d.tiles_h * d.tiles_w * d.nblk >= 256;
 }
 
 template <int TM, bool FLIP>
-static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
+static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s,
+                            int nr = 0) {
+  if (nr) {  // fp32 operands (pick_dtile)
+    if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2>), grid, dim3(256), shm, s, p);
+    else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4>), grid, dim3(256), shm, s, p);
+    else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8>), grid, dim3(256), shm, s, p);
+    return;
+  }
   switch (tn) {
 #define CASE(T) \
   case T:                                                                         \
@@ -1361,7 +1482,8 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
 }
 
 static size_t dconv_shm(const DTile& d) {
-  return (size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) * sizeof(float);
+  return ((size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) + (size_t)d.nr * 9 * d.cs4 * 4) *
+         sizeof(float);
 }
 
 template <int TM, bool FLIP>
@@ -1390,13 +1512,13 @@ static int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uin
   p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
   p.stats = stats;
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
-  const size_t shm = (size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) * sizeof(float);
+  const size_t shm = dconv_shm(d);
   if (d.tm == 4) {
-    if (flip) dconv_launch_tn<4, true>(p, d.tn, grid, shm, s);
-    else dconv_launch_tn<4, false>(p, d.tn, grid, shm, s);
+    if (flip) dconv_launch_tn<4, true>(p, d.tn, grid, shm, s, d.nr);
+    else dconv_launch_tn<4, false>(p, d.tn, grid, shm, s, d.nr);
   } else {
-    if (flip) dconv_launch_tn<2, true>(p, d.tn, grid, shm, s);
-    else dconv_launch_tn<2, false>(p, d.tn, grid, shm, s);
+    if (flip) dconv_launch_tn<2, true>(p, d.tn, grid, shm, s, d.nr);
+    else dconv_launch_tn<2, false>(p, d.tn, grid, shm, s, d.nr);
   }
   return check_launch(fn);
 }
@@ -1572,12 +1694,13 @@ int vae2_wgrad_flush(void* stream) {
 }
 
 int vae2_conv2d_set_algo(int algo) {
-  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8);
+  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) + (g_dconv_nr ? 0 : 16);
   const int a = algo & 7;
-  if (algo >= 0 && algo <= 15 && a <= 6 && a != 3) {
+  if (algo >= 0 && algo <= 31 && a <= 6 && a != 3) {
     g_conv_algo = a & 3;
     g_wide_tiles = a < 4;
     g_ksplit = !(algo & 8);
+    g_dconv_nr = !(algo & 16);
   }
   return prev;
 }
@@ -1594,7 +1717,10 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
   if (!xd || !yd || !buf || len <= 0) return -22;
   if (dconv_use(xd, yd, k, stride, pad, (const float*)16)) {
     DTile d = pick_dtile(xd, yd);
-    snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
+    if (d.nr)
+      snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false, false, %d>", d.tm, d.tn, d.nr);
+    else
+      snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
     return 0;
   }
   Tile t = pick_igemm_tile(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4), 1);
@@ -1762,7 +1888,7 @@ int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
       if (rc) return rc;
       continue;
     }
-    const DTile d = pick_dtile(ad, od);
+    const DTile d = pick_dtile(ad, od, false);
     const uint32_t wb = (uint32_t)((fwd ? vae2_conv2d_packed_size(od->c, ad->c, J.k, 0)
                                         : vae2_conv2d_packed_size(ad->c, od->c, J.k, 1)) * 4);
     int k = 0;

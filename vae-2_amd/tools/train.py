@@ -199,12 +199,12 @@ def main(argv=None):
             sampler.set_epoch(epoch)
         if extra_sampler is not None and extra_sampler is not sampler:
             extra_sampler.set_epoch(epoch)
-        if epoch >= config.TRAIN.END_EPOCH:  # extra epochs restart the schedule (train.py:300-306)
+        if epoch >= config.TRAIN.END_EPOCH:  # train.py:300-306
+            # EXTRA_LR reaches adversarial_train as base_lr, which only logs it: the
+            # reference's adjust_learning_rate call is commented out (function.py:525-528),
+            # so the optimizers keep training at TRAIN.LR in the extra epochs too
             ep_args = (epoch - config.TRAIN.END_EPOCH, config.TRAIN.EXTRA_EPOCH, epoch_iters,
                        config.TRAIN.EXTRA_LR, extra_iters, extra_loader)
-            for opt in (optimizer, optimizer_D):
-                if opt is not None:
-                    opt.set_lr(config.TRAIN.EXTRA_LR)
         else:
             ep_args = (epoch, config.TRAIN.END_EPOCH, epoch_iters, config.TRAIN.LR, num_iters,
                        loader)

@@ -32,7 +32,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, prof
 from ._lib import Act, call
 from .ops import (_WS_HOLD, _all_reduce_sums, _bn_group, _empty, _grad_sink, act_of, as_act,
                   new_act, packed_weight_cols, ptr, stream_ptr, wgrad_batch)
@@ -94,6 +94,10 @@ class _Heads(torch.autograd.Function):
                 z = new_act((yj.shape[0], yj.shape[1], yj.shape[2], C), yj)
                 yjp, yja = act_of(yj)
                 zp, za = act_of(z)
+                if prof.active():
+                    pj = yja.n * yja.h * yja.w
+                    prof.note(2.0 * pj * C * yja.c, 4.0 * (pj * yja.c + pj * C + C * yja.c),
+                              prof.conv_label("head fwd", yja.c, C, 1, 1, yja.h, yja.w))
                 call("vae2_conv2d_fwd", yjp, ctypes.byref(yja),
                      ptr(packed_weight_cols(w, split, j, 0)), None, zp, ctypes.byref(za), 1, 1, 0,
                      0.0, None, s)
@@ -103,6 +107,11 @@ class _Heads(torch.autograd.Function):
             y = _empty((-(-C // 64) * n * H * W * 64,), x0)  # B64 layout (heads.hip)
             yp, ya = ptr(y), yshape
             stats = _empty((2 * rows * C,), x0) if training[k] else None
+            P0 = n * H * W
+            if prof.active():  # W0 x0 on MFMA + the upsampled branch products, y written once
+                prof.note(2.0 * P0 * C * split[0],
+                          4.0 * (P0 * split[0] + P0 * C + sum(z.numel() for z, _, _ in zs)),
+                          prof.conv_label("head upsum", split[0], C, 1, 1, H, W))
             call("vae2_conv1x1_upsum_fwd", x0p, ctypes.byref(x0a),
                  ptr(packed_weight_cols(w, split, 0, 0)), ptr(b), nb - 1, ups, upds, yp,
                  ctypes.byref(ya), ptr(stats), s)
@@ -135,6 +144,9 @@ class _Heads(torch.autograd.Function):
                      ptr(bn.running_var), float(bn.eps), C, ptr(save), s)
             o = out[..., ncls * k:ncls * (k + 1)]
             op, oa = act_of(o)
+            if prof.active():
+                prof.note(2.0 * P0 * C * ncls, 4.0 * (P0 * C + P0 * ncls),
+                          prof.conv_label("head out", C, ncls, 1, 1, H, W))
             call("vae2_head_out_fwd", yp, ctypes.byref(ya), ptr(save), ptr(w2), ptr(b2), ncls, op,
                  ctypes.byref(oa), s)
             ys_saved.append(y)
@@ -179,6 +191,11 @@ class _Heads(torch.autograd.Function):
             btsink, btret = _grad_sink(beta, nbt)
             w2sink, w2ret = _grad_sink(w2, nw2)
             b2sink, b2ret = _grad_sink(b2, nb2)
+            P0 = ys[0].shape[0] * ys[0].shape[1] * ys[0].shape[2]
+            Hh, Ww = ys[0].shape[1], ys[0].shape[2]
+            if prof.active():  # the 270 -> 3 conv's weight gradient + BN backward sums
+                prof.note(2.0 * P0 * C * ncls, 4.0 * (P0 * C + P0 * ncls),
+                          prof.conv_label("head out wgrad", C, ncls, 1, 1, Hh, Ww))
             call("vae2_head_out_bwd_reduce", yp, ctypes.byref(ya), ptr(save), ptr(w2), ncls, dkp,
                  ctypes.byref(dka), ptr(lsums), ptr(gsink), ptr(btsink), ptr(w2sink),
                  ptr(b2sink), ptr(ws), wsz, s)
@@ -186,6 +203,9 @@ class _Heads(torch.autograd.Function):
             dy = new_act((*ys[0].shape[:3], C), y)
             dyp, dya = act_of(dy)
             bsink, bret = _grad_sink(b, nbias)
+            if prof.active():  # the 270 -> 3 conv's data gradient + BN backward, dL/dy written
+                prof.note(2.0 * P0 * C * ncls, 4.0 * (2 * P0 * C + P0 * ncls),
+                          prof.conv_label("head out dgrad", C, ncls, 1, 1, Hh, Ww))
             call("vae2_head_out_bwd_apply", yp, ctypes.byref(ya), ptr(save), ptr(gamma), ptr(w2),
                  ncls, dkp, ctypes.byref(dka), ptr(gsums), ctx.count, dyp, ctypes.byref(dya),
                  ptr(bsink), ptr(ws), wsz, s)
@@ -200,6 +220,8 @@ class _Heads(torch.autograd.Function):
                 gacts = (Act * 3)(*[ga for _, _, ga in gs[1:]])
                 usz = lib.vae2_upsample_bilinear_bwd_multi_ws_size(ctypes.byref(dya), nb - 1, gacts)
                 uws = _empty((usz,), y)
+                if prof.active():
+                    prof.note(0.0, 4.0 * (dy.numel() + sum(g.numel() for g, _, _ in gs[1:])))
                 call("vae2_upsample_bilinear_bwd_multi", dyp, ctypes.byref(dya), nb - 1, gptrs,
                      gacts, ptr(uws), usz, s)
             c0 = 0
@@ -212,6 +234,10 @@ class _Heads(torch.autograd.Function):
                         wsz2 = lib.vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xja),
                                                                   ctypes.byref(ga), 1)
                         ws2 = _empty((max(wsz2, 1),), xj)
+                        if prof.active():
+                            pj = xja.n * xja.h * xja.w
+                            prof.note(2.0 * pj * xja.c * C, 4.0 * (pj * xja.c + pj * C + C * xja.c),
+                                      prof.conv_label("head wgrad", xja.c, C, 1, 1, xja.h, xja.w))
                         call("vae2_conv2d_bwd_weight_ld", xjp, ctypes.byref(xja), gp,
                              ctypes.byref(ga), ctypes.c_void_p(wsink.data_ptr() + 4 * c0), C,
                              None, 1, 1, 0, 1, ptr(ws2), wsz2, s)
@@ -221,6 +247,10 @@ class _Heads(torch.autograd.Function):
                         if first:
                             dxs[j] = new_act(tuple(xj.shape), xj)
                         dxp, dxa = act_of(dxs[j])
+                        if prof.active():
+                            pj = dxa.n * dxa.h * dxa.w
+                            prof.note(2.0 * pj * dxa.c * C, 4.0 * (pj * dxa.c + pj * C + C * dxa.c),
+                                      prof.conv_label("head dgrad", dxa.c, C, 1, 1, dxa.h, dxa.w))
                         call("vae2_conv2d_bwd_data", gp, ctypes.byref(ga),
                              ptr(packed_weight_cols(w, split, j, 1)), dxp, ctypes.byref(dxa), 1,
                              1, 0, 0.0 if first else 1.0, s)

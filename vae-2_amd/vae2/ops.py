@@ -301,13 +301,14 @@ class ConvGroup:
     a queued job writes t's storage (the caller flushes before touching it)."""
 
     def __init__(self):
-        self.jobs, self.hold, self.outs = [], [], set()
+        self.jobs, self.hold, self.outs, self.notes = [], [], set(), []
 
     def add(self, kind, x, xa, wp, bias, y, ya, spec, beta=0.0, stats=None):
         self.jobs.append(_lib.ConvJob(kind, spec.k, spec.stride, spec.pad, x, xa, ptr(wp),
                                       ptr(bias), y, ya, beta, ptr(stats)))
         self.hold.append((wp, bias, stats))
         self.outs.add(y.value if isinstance(y, ctypes.c_void_p) else int(y))
+        self.notes.append(prof.take())  # the job's algorithmic work travels with it
 
     def pending(self, t):
         return t is not None and t.data_ptr() in self.outs
@@ -315,9 +316,28 @@ class ConvGroup:
     def flush(self):
         if not self.jobs:
             return
-        arr = (_lib.ConvJob * len(self.jobs))(*self.jobs)
-        call("vae2_conv2d_multi", len(self.jobs), arr, stream_ptr())
-        self.jobs, self.hold, self.outs = [], [], set()
+        if prof.active() and not _lib.load().vae2_conv2d_set_grouping(0):
+            # profiling, jobs launched one by one anyway (grouping off): one call per job,
+            # so each call's time and work are its own kernel's
+            for job, work in zip(self.jobs, self.notes):
+                prof.put(work)
+                call("vae2_conv2d_multi", 1, (_lib.ConvJob * 1)(job), stream_ptr())
+        else:
+            if prof.active():
+                _lib.load().vae2_conv2d_set_grouping(1)
+                prof.put(_merge(self.notes))
+            arr = (_lib.ConvJob * len(self.jobs))(*self.jobs)
+            call("vae2_conv2d_multi", len(self.jobs), arr, stream_ptr())
+        self.jobs, self.hold, self.outs, self.notes = [], [], set(), []
+
+
+def _merge(notes):
+    """One note for a grouped launch: work summed, layer shapes joined."""
+    notes = [n for n in notes if n is not None]
+    if not notes:
+        return None
+    return (sum(n[0] for n in notes), sum(n[1] for n in notes),
+            " + ".join(n[2] for n in notes if n[2]))
 
 
 def _conv_fwd_queued(group, x, weight, bias, spec, stats):
@@ -368,7 +388,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
     wsink, wret = _grad_sink(weight, need_w)
     bsink, bret = _grad_sink(bias, need_b)
     if wsink is not None or bsink is not None:
-        if wsink is None:  # weight frozen but bias trained: still need a dW target
+        tmp_w = wsink is None
+        if tmp_w:  # weight frozen but bias trained: still need a dW target
             wsink = torch.zeros_like(weight)
         size = _lib.load().vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xa), ctypes.byref(dya),
                                                           spec.k)
@@ -378,7 +399,11 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya), ptr(wsink),
              ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
         if _WGRAD_BATCH[0]:
+            # the deferred reduction writes wsink at the flush: a temporary dW target
+            # must outlive it like the workspace
             _WS_HOLD.append(ws)
+            if tmp_w:
+                _WS_HOLD.append(wsink)
     dx = None
     if need_dx:
         link = spec.x_link

@@ -58,19 +58,47 @@ def family(kernel):
     return "other"
 
 
+_ABI_FAMILY = (("conv_dgrad", "bwd_data"), ("conv_wgrad", "bwd_weight"), ("conv_fwd", "conv2d"),
+               ("heads", "head_|upsum"), ("batchnorm", "bn_"))
+
+
+def _abi_family(name):
+    """Family of a C-ABI call that launched no kernel (its work still counts)."""
+    for f, key in _ABI_FAMILY:
+        if re.search(key, name):
+            return f
+    return "other"
+
+
 def active():
     return _ACTIVE
 
 
 def note(flops=0.0, nbytes=0.0, shape=None):
-    """Annotate the next C-ABI call with its algorithmic work (no-op unless profiling);
-    several notes before one call (a grouped launch) add up, their shapes joined by ' + '."""
+    """Annotate the NEXT C-ABI call with its own algorithmic work (no-op unless profiling).
+    Every note belongs to exactly one call: a note still pending when another is made is
+    counted in StepProfiler.conflicts (bench.py reports it; the profiler test asserts 0) and
+    replaced.  A launch queued for a later call carries its note there (take / put)."""
     if _ACTIVE is not None:
         if _ACTIVE.pending is not None:
-            f0, b0, s0 = _ACTIVE.pending
-            shape = s0 if shape is None else (shape if s0 is None else f"{s0} + {shape}")
-            flops, nbytes = f0 + flops, b0 + nbytes
+            _ACTIVE.conflicts += 1
         _ACTIVE.pending = (float(flops), float(nbytes), shape)
+
+
+def take():
+    """Pop the pending note (a queued launch: ops.ConvGroup stores it with the job)."""
+    if _ACTIVE is None:
+        return None
+    w, _ACTIVE.pending = _ACTIVE.pending, None
+    return w
+
+
+def put(work):
+    """Re-arm a note taken earlier for the call about to issue its launch."""
+    if _ACTIVE is not None and work is not None:
+        if _ACTIVE.pending is not None:
+            _ACTIVE.conflicts += 1
+        _ACTIVE.pending = work
 
 
 def conv_label(kind, cin, cout, k, stride, h, w):
@@ -92,6 +120,7 @@ class StepProfiler:
     def __init__(self):
         self.records = []  # (abi fn, kernels label, start ev, end ev, flops, bytes, shape)
         self.pending = None
+        self.conflicts = 0  # notes overwritten before their call (must stay 0)
         self._buf = ctypes.create_string_buffer(1 << 14)
 
     def __enter__(self):
@@ -122,8 +151,8 @@ class StepProfiler:
         n = lib.vae2_kernel_log_read(self._buf, len(self._buf))
         work = self.pending or (0.0, 0.0, None)
         self.pending = None
-        if n > 0:
-            self.records.append((name, self._buf.value.decode(), s, e) + work)
+        # a call that launched nothing keeps its record (zero time): its work still counts
+        self.records.append((name, self._buf.value.decode() if n > 0 else "", s, e) + work)
         return rc
 
     def summary(self, steps):
@@ -135,16 +164,17 @@ class StepProfiler:
         shp = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
         total = 0.0
         for name, kernels, s, e, flops, nbytes, shape in self.records:
-            ms = s.elapsed_time(e)
+            ms = s.elapsed_time(e) if kernels else 0.0
             total += ms
             ks = kernels.split(";")
-            for d, key in ((ker, kernels), (fam, family(ks[0]))):
+            fk = family(ks[0]) if kernels else _abi_family(name)
+            for d, key in ((ker, kernels or name), (fam, fk)):
                 d[key][0] += ms
                 d[key][1] += 1
                 d[key][2] += flops
                 d[key][3] += nbytes
-            if shape is not None:
-                d = shp[shape]
+            if shape is not None:  # one row per (layer shape, launched kernel instance)
+                d = shp[f"{shape} | {kernels or '(no launch)'}"]
                 d[0] += ms
                 d[1] += 1
                 d[2] += flops
@@ -168,7 +198,7 @@ class StepProfiler:
             return out
 
         return {"kernel_ms_per_step": round(total / steps, 3), "families": rows(fam),
-                "kernels": rows(ker), "conv_shapes": rows(shp)}
+                "kernels": rows(ker), "conv_shapes": rows(shp), "note_conflicts": self.conflicts}
 
     def dominant(self, steps):
         """The single kernel (one instantiation) with the most time: its launches'
@@ -176,7 +206,7 @@ class StepProfiler:
         torch.cuda.synchronize()
         agg = defaultdict(lambda: [0.0, 0, 0.0, 0.0])
         for name, kernels, s, e, flops, nbytes, shape in self.records:
-            if ";" in kernels:
+            if ";" in kernels or not kernels:
                 continue
             a = agg[kernels]
             a[0] += s.elapsed_time(e)
