@@ -319,12 +319,17 @@ def test_stage4_module_at_bench_geometry(bench_step):
     gouts = [torch.randn(o.shape, generator=g) for o in o64]
     torch.autograd.backward(o64, [go.double() for go in gouts])
     torch.autograd.backward(o32, gouts)
-    # the reference's own sensitivity: fp64 with 1e-6 relative noise on the inputs (every
-    # ReLU / fuse mask an fp32 rounding can flip is a discontinuity of the gradient)
-    m64p = copy.deepcopy(mod).double()
-    x64p = [(x.double() * (1 + 1e-6 * torch.randn(x.shape, generator=g, dtype=torch.float64)))
-            .requires_grad_() for x in xs]
-    torch.autograd.backward(_ref_block_module(m64p, x64p), [go.double() for go in gouts])
+    # the reference's own sensitivity: fp64 runs with 1e-6 relative noise on the inputs
+    # (the fp32 forwards here are 2-8e-7 from fp64; every ReLU / fuse mask such an error
+    # flips moves the gradients upstream of it by ~1e-3: at 1.2M pre-activations per
+    # branch that is a lottery of ~1 flip per run), the largest distance over 4 draws
+    sens = []
+    for _ in range(4):
+        m64p = copy.deepcopy(mod).double()
+        x64p = [(x.double() * (1 + 1e-6 * torch.randn(x.shape, generator=g, dtype=torch.float64)))
+                .requires_grad_() for x in xs]
+        torch.autograd.backward(_ref_block_module(m64p, x64p), [go.double() for go in gouts])
+        sens.append((m64p, x64p))
     mg = copy.deepcopy(mod).to(DEV)
     from vae2 import ops
     xg = []
@@ -340,12 +345,14 @@ def test_stage4_module_at_bench_geometry(bench_step):
     errs = [max_rel(_nchw(o), r) for o, r in zip(og, o64)]
     assert max(errs) < 1e-4, errs
 
-    rows = [(f"x{i}.grad", rel(_nchw(a.grad), b.grad), rel(c.grad, b.grad), rel(d.grad, b.grad))
-            for i, (a, b, c, d) in enumerate(zip(xg, x64, x32, x64p))]
-    rows += [(n, rel(p.grad, p64.grad), rel(p32.grad, p64.grad), rel(pp.grad, p64.grad))
-             for (n, p), (_, p64), (_, p32), (_, pp) in
-             zip(mg.named_parameters(), m64.named_parameters(), m32.named_parameters(),
-                 m64p.named_parameters())]
+    rows = [(f"x{i}.grad", rel(_nchw(a.grad), b.grad), rel(c.grad, b.grad),
+             max(rel(xp[i].grad, b.grad) for _, xp in sens))
+            for i, (a, b, c) in enumerate(zip(xg, x64, x32))]
+    sp = [dict(m.named_parameters()) for m, _ in sens]
+    rows += [(n, rel(p.grad, p64.grad), rel(p32.grad, p64.grad),
+              max(rel(d[n].grad, p64.grad) for d in sp))
+             for (n, p), (_, p64), (_, p32) in
+             zip(mg.named_parameters(), m64.named_parameters(), m32.named_parameters())]
     for r in rows:
         print(f"{r[0]:40s} hip {r[1]:.3e}  cpu32 {r[2]:.3e}  fp64(x+1e-6) {r[3]:.3e}")
     print("outputs max-rel: hip", [f"{e:.2e}" for e in errs], "cpu32",

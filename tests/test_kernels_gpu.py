@@ -144,22 +144,22 @@ def test_direct_conv3x3_valu_remainder(shape):
     y_ref.backward(gy)
     cg = nn.Conv2d(cin, cout, 3, 1, 1, bias=bias).to(DEV)
     cg.load_state_dict(conv.state_dict())
+    from test_bench_instances_gpu import Recorder
     lib = _lib.load()
     prev = lib.vae2_conv2d_set_algo(2)
-    lib.vae2_kernel_log(1)
     try:
         xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
         with torch.no_grad():
             xg.copy_(nhwc(x.detach()).to(DEV))
         xg.requires_grad_(True)
-        lib.vae2_kernel_log_read(None, 0)
-        yg = ops.conv(xg, cg)
-        yg.backward(nhwc(gy).to(DEV))
-        torch.cuda.synchronize()
-        import ctypes
-        buf = ctypes.create_string_buffer(1 << 14)
-        lib.vae2_kernel_log_read(buf, len(buf))
-        names = buf.value.decode().split(";")
+        gpad = ops.new_act((n, h, w, cout), xg)  # padded pixel stride, as in the model
+        with torch.no_grad():
+            gpad.copy_(nhwc(gy).to(DEV))
+        with Recorder() as rec:  # launch log read in the calling thread (autograd's too)
+            yg = ops.conv(xg, cg)
+            yg.backward(gpad)
+            torch.cuda.synchronize()
+        names = [k for _, _, ks in rec.calls for k in ks]
         # BN statistics from the remainder epilogue (conv_bn: running mean / var)
         bn, bg = nn.BatchNorm2d(cout, momentum=0.5), nn.BatchNorm2d(cout, momentum=0.5).to(DEV)
         with torch.no_grad():
@@ -167,7 +167,6 @@ def test_direct_conv3x3_valu_remainder(shape):
             bn(conv(x.detach()))
         torch.cuda.synchronize()
     finally:
-        lib.vae2_kernel_log(0)
         lib.vae2_conv2d_set_algo(prev)
     for c in (cout, cin):
         nr = c % 16

@@ -20,6 +20,25 @@ HEADERS = ["common.h", os.path.join("..", "..", "include", "vae2_hip.h")]
 ARCH = os.environ.get("VAE2_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
          "-Wno-unused-function", "-munsafe-fp-atomics"]
+# per-source extras: no SLP vectorisation in the conv kernels (it packs independent f32
+# FMAs beside the MFMAs into v_pk_fma_f32 + operand moves, which cost issue slots there)
+EXTRA = {"conv.hip": ["-fno-slp-vectorize"]}
+# conv.hip is compiled as four objects (VAE2_CONV_PART 0..3: pack + C-ABI dispatch, gather
+# kernels, direct 3x3 kernels, weight-gradient kernels) so its instantiations build in
+# parallel
+PARTS = {"conv.hip": 4}
+
+
+def _units():
+    out = []
+    for src in SOURCES:
+        n = PARTS.get(src, 0)
+        base = os.path.splitext(src)[0]
+        if n:
+            out += [(src, f"{base}_p{i}.o", [f"-DVAE2_CONV_PART={i}"]) for i in range(n)]
+        else:
+            out.append((src, base + ".o", []))
+    return out
 
 
 def hipcc():
@@ -36,12 +55,13 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
-    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+def _compile(unit):
+    src, oname, defs = unit
+    obj = os.path.join(BUILD, oname)
     deps = [os.path.join(HERE, src)] + [os.path.join(HERE, h) for h in HEADERS]
     if not _newer(obj, deps):
         return obj, None
-    cmd = [hipcc()] + FLAGS + ["-c", os.path.join(HERE, src), "-o", obj]
+    cmd = [hipcc()] + FLAGS + EXTRA.get(src, []) + defs + ["-c", os.path.join(HERE, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
@@ -53,8 +73,9 @@ def build(verbose=True, force=False):
     if force:
         for f in os.listdir(BUILD):
             os.remove(os.path.join(BUILD, f))
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        results = list(ex.map(_compile, SOURCES))
+    units = _units()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(units))) as ex:
+        results = list(ex.map(_compile, units))
     errors = [e for _, e in results if e]
     if errors:
         raise RuntimeError("HIP compile failed:\n" + "\n".join(errors))

@@ -31,6 +31,16 @@
 #define VAE2_ABLATE 0
 #endif
 
+// The build compiles this file once per part (-DVAE2_CONV_PART=0..3, in parallel): each
+// part defines the host launchers of one kernel family, so the kernel templates are
+// instantiated (and compiled) in that part only.  0: weight packing and the forward /
+// data-gradient C ABI; 1: gather implicit GEMM; 2: direct 3x3 (+ grouped launches);
+// 3: weight gradients.  Without the macro everything is in one translation unit.
+#ifndef VAE2_CONV_PART
+#define VAE2_CONV_PART -1
+#endif
+#define VAE2_PART(n) (VAE2_CONV_PART < 0 || VAE2_CONV_PART == (n))
+
 namespace vae2 {
 
 
@@ -45,6 +55,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
 }
 
 
+#if VAE2_PART(0)
 // ------------------------------------------------------------ weight pack ----
 // mode 0: out[n][t][c4] = w[n][c][t]         n < round_up(cout,64), c4 < round_up(cin,4)
 // mode 1: out[n][t][c4] = w[c][n][t]         n < round_up(cin,64),  c4 < round_up(cout,4)
@@ -95,6 +106,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pa
   }
 }
 
+#endif  // VAE2_PART(0)
 // ------------------------------------------------------------ igemm ----
 struct IGemm {
   const float* a;  // gathered activation (NHWC)
@@ -460,7 +472,9 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   const int rtrow = wave * (TM / 2) + ((rl >> 4) >> 1), rtcol = ((rl >> 4) & 1) * 16 + (rl & 15);
   const int rbase = ((rtrow + 1) * LW + rtcol + 1) * csp;
   float* const rw = tile + LH * LW * csp;
-  const int rws = 9 * p.cs4 * 4;  // floats per remainder channel in rw
+  // floats per remainder channel in rw: the K steps of an even number of chunks (the main
+  // loop runs chunks in pairs), zero past the slab's 9 x qs steps
+  const int rws = ((9 * p.cs4 + 7) >> 3) * 32;
   float racc[NRL > 0 ? NRL : 1];
 #pragma unroll
   for (int j = 0; j < NRL; ++j) racc[j] = 0.f;
@@ -470,13 +484,14 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const int qs = Q - q0 < p.cs4 ? Q - q0 : p.cs4;
     // ---- stage the halo tile of this slab (zero outside the image / past a_c) ----
     __syncthreads();
-    if constexpr (NR > 0) {  // remainder weights of the slab, tap-major, FLIP applied
-      const int per = 9 * qs * 4;
+    if constexpr (NR > 0) {  // remainder weights of the slab [j][(tap, quad)][4], FLIP
+      const int per = ((9 * qs + 7) >> 3) * 32;  // whole chunk pairs: zero tail
       for (int i = threadIdx.x; i < NR * per; i += 256) {
         const int j = i / per, rem = i - j * per;
         const int t = rem / (qs * 4), c = rem - t * (qs * 4);
         const int tl = FLIP ? 8 - t : t;
-        rw[j * rws + t * (qs * 4) + c] = p.w[(int64_t)(BN + j) * kk4 + tl * p.a_c4 + q0 * 4 + c];
+        rw[j * rws + rem] =
+            t < 9 ? p.w[(int64_t)(n0 + BN + j) * kk4 + tl * p.a_c4 + q0 * 4 + c] : 0.f;
       }
     }
     // thread -> (channel quad q = tid % qs, pixels pb, pb + pstride, ...); SB loads in
@@ -518,8 +533,15 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     __syncthreads();
     // ---- 9 taps x qs quads of K from LDS ----
     const int nch = (9 * qs + 3) >> 2;
-    int t = 0, q = g;
-    while (q >= qs) { q -= qs; ++t; }
+    // (tap, quad) of this lane group's next K chunk: q advances by 4 quads per chunk;
+    // the carry into the tap is at most 4 (qs >= 1), taken branch-free
+    int t = (g >= qs) + (g >= 2 * qs) + (g >= 3 * qs), q = g - t * qs;
+    auto step = [&]() {
+      const int nq = q + 4;
+      const int dt = (nq >= qs) + (nq >= 2 * qs) + (nq >= 3 * qs) + (nq >= 4 * qs);
+      q = nq - dt * qs;
+      t += dt;
+    };
     auto load = [&](f4* fa, f4* fb) {
       const bool tv = t < 9;
       const int tt = tv ? t : 0;
@@ -532,29 +554,28 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       const uint32_t woff = tv ? (uint32_t)(tl * p.a_c4 + (q0 + q) * 4) * 4u : kOOB;
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
-      q += 4;
-      while (q >= qs) { q -= qs; ++t; }
+      step();
     };
-    // the remainder's share of chunk ch: its 4 (tap, quad) K steps (wave-uniform)
-    auto rem = [&](int ch) {
+    // the remainder's share of a chunk: its 4 (tap, quad) K steps, wave-uniform counters,
+    // branch-free (steps past the 9 taps read tap 8 against the zeroed tail of rw)
+    int rkq = 0, rt = 0, rq = 0;
+    auto rem = [&]() {
       if constexpr (NR > 0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int kq = ch * 4 + u;
-          if (kq < 9 * qs) {
-            const int t = kq / qs, q = kq - t * qs;
-            const int dh = (t >= 3) + (t >= 6) - 1, dw = t - 3 * (dh + 1) - 1;
-            const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + (dh * LW + dw) * csp + 4 * q]);
+          const int tc = rt < 9 ? rt : 8;
+          const int dh = (tc >= 3) + (tc >= 6) - 1, dw = tc - 3 * (dh + 1) - 1;
+          const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + (dh * LW + dw) * csp + 4 * rq]);
 #pragma unroll
-            for (int j = 0; j < NRL; ++j) {
-              const f4 wv = *reinterpret_cast<const f4*>(
-                  &rw[(rh * NRL + j) * rws + t * (qs * 4) + 4 * q]);
-              racc[j] = __builtin_fmaf(xv[0], wv[0], racc[j]);
-              racc[j] = __builtin_fmaf(xv[1], wv[1], racc[j]);
-              racc[j] = __builtin_fmaf(xv[2], wv[2], racc[j]);
-              racc[j] = __builtin_fmaf(xv[3], wv[3], racc[j]);
-            }
+          for (int j = 0; j < NRL; ++j) {
+            const f4 wv = *reinterpret_cast<const f4*>(&rw[(rh * NRL + j) * rws + 4 * rkq]);
+            racc[j] = __builtin_fmaf(xv[0], wv[0], racc[j]);
+            racc[j] = __builtin_fmaf(xv[1], wv[1], racc[j]);
+            racc[j] = __builtin_fmaf(xv[2], wv[2], racc[j]);
+            racc[j] = __builtin_fmaf(xv[3], wv[3], racc[j]);
           }
+          ++rkq;
+          if (++rq == qs) { rq = 0; ++rt; }
         }
       }
     };
@@ -563,10 +584,10 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       for (int ch = 0; ch < nch; ch += 2) {
         load(fa1, fb1);
         mma(fa0, fb0);
-        rem(ch);
+        rem();
         load(fa0, fb0);
         mma(fa1, fb1);
-        rem(ch + 1);
+        rem();
       }
     } else {  // bf16 operands: one 16x16x32 MFMA per chunk pair
       load(fa0, fb0);
@@ -618,7 +639,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   if constexpr (NR > 0) {
     const int oh = oh0 + rtrow, ow = ow0 + rtcol;
     const bool in = oh < p.img_h && ow < p.img_w;
-    const int nb = BN + rh * NRL;
+    const int nb = n0 + BN + rh * NRL;
     float* yrow = p.y + (int64_t)((img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0)) * p.y_ps + nb;
 #pragma unroll
     for (int j = 0; j < NRL; ++j) {
@@ -719,7 +740,15 @@ struct Tile {
 // at least 16 chunks of 16), giving 4x the workgroups.
 static int64_t igemm_rows_per_block(const Tile& t) { return (t.ks > 1 ? 16 : 64) * t.tm; }
 
-static int g_wide_tiles = 1;
+#if VAE2_PART(0)
+int g_wide_tiles = 1;
+int g_ksplit = 1;    // vae2_conv2d_set_algo bit 8 disables the K split (A/B tests)
+int g_bf16 = 0;      // vae2_conv2d_set_mfma_bf16: bf16 MFMA operands (fp32 accumulate)
+int g_conv_algo = 0; // 0 auto, 1 gather kernel only, 2 direct wherever legal
+int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
+#else
+extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr;
+#endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
 // 32 rows, so the activation rows are re-read by 2 column blocks instead of 5.
@@ -748,8 +777,6 @@ static Tile pick_tile(int64_t M, int N, bool wide = false) {
   return t;
 }
 
-static int g_ksplit = 1;  // vae2_conv2d_set_algo bit 8 disables the K split (A/B tests)
-static int g_bf16 = 0;    // vae2_conv2d_set_mfma_bf16: bf16 MFMA operands (fp32 accumulate)
 
 static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   const bool wide = wide_ok(M, N, taps);
@@ -760,6 +787,13 @@ static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   return t;
 }
 
+static bool vec_ok(const float* a, int ps) {
+  return ((uintptr_t)a % 16 == 0) && (ps % 4 == 0);
+}
+
+int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls = 1);
+
+#if VAE2_PART(1)
 template <int TM, bool VEC, int ROLE, int KS = 1>
 static void launch_tn(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
   switch (tn) {
@@ -800,12 +834,8 @@ static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
   else launch_tn<1, VEC, ROLE>(p, t.tn, grid, s);
 }
 
-static bool vec_ok(const float* a, int ps) {
-  return ((uintptr_t)a % 16 == 0) && (ps % 4 == 0);
-}
-
 // ncls > 1: p.cls[0..ncls) hold the parity classes; the grid covers the largest one.
-static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls = 1) {
+int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls) {
   int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
   if (ncls > 1) {
     M = 0;
@@ -835,6 +865,8 @@ static int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int n
   }
   return check_launch(fn);
 }
+
+#endif  // VAE2_PART(1)
 
 static int64_t igemm_rows(int64_t M, int N, int taps, int k4) {
   Tile t = pick_igemm_tile(M, N, taps, k4, 1);
@@ -1227,6 +1259,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   }
 }
 
+#if VAE2_PART(3)
 // dw[co][ci][kh][kw] (+)= sum_s part[s][co][(kh*k+kw)*cin4 + ci]
 // Block = 32 slab columns x 8 split groups: thread (g, col) sums splits g, g+8, ...
 // (unrolled: its loads are independent), the 8 group sums are combined in LDS in a fixed
@@ -1264,6 +1297,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
+#endif  // VAE2_PART(3)
 // Deferred reductions (vae2_wgrad_defer / vae2_wgrad_flush): the weight gradients of
 // one BatchNorm depth level (the lock-stepped branch convs, a head's branch blocks) share
 // one reduce launch; blocks are partitioned between the jobs by prefix.
@@ -1279,6 +1313,7 @@ struct WRMulti {
   int n;
 };
 
+#if VAE2_PART(3)
 __global__ __launch_bounds__(256) void wgrad_reduce_multi_kernel(WRMulti m) {
   int i = 0;
   while (i + 1 < m.n && (int)blockIdx.x >= m.j[i + 1].blk0) ++i;
@@ -1310,6 +1345,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_multi_kernel(WRMulti m) {
   const int64_t o = (int64_t)co * J.ld + ci * kk + t;
   J.dw[o] = J.accumulate ? J.dw[o] + s : s;
 }
+
+#endif  // VAE2_PART(3)
 
 struct WRQueued {
   WRJob job;
@@ -1343,6 +1380,7 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   return t;
 }
 
+#if VAE2_PART(3)
 template <int TM>
 static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)3 * TM * 4 * 4 * 64 * sizeof(float) / 4 * tn;  // 3 waves x NV x 64
@@ -1365,6 +1403,8 @@ static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
       break;
   }
 }
+
+#endif  // VAE2_PART(3)
 
 // ------------------------------------------------------------- checks ----
 static bool conv_shapes_ok(const vae2_act* xd, const vae2_act* yd, int k, int stride, int pad) {
@@ -1395,14 +1435,12 @@ static uint32_t act_bytes(const vae2_act* d) {
 using namespace vae2;
 
 // ---------------------------------------------- direct 3x3: host dispatch ----
-static int g_conv_algo = 0;  // 0 auto, 1 gather kernel only, 2 direct wherever legal
 
 struct DTile {
   int tm, tn, nblk, cs4, tiles_h, tiles_w;
   int nr = 0;  // output channels on the VALU beside the MFMA tiles (dconv3_body NR)
 };
 
-static int g_dconv_nr = 0;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
 
 static bool dconv_legal(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
                         const float* a) {
@@ -1419,8 +1457,11 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   d.tn = t.tn;
   d.nblk = t.nblk;
   const int N = (int)yd->c, tn = N / 16, nr = N % 16;
+  // (auto: 16 + 2 only — the 36 / 72-channel forms measured slower than their padded
+  //  MFMA tiles; algo 2 takes all three, for the tests)
   if (remainder && g_dconv_nr && !g_bf16 &&
-      ((tn == 1 && nr == 2) || (tn == 2 && nr == 4) || (tn == 4 && nr == 8))) {
+      ((tn == 1 && nr == 2) ||
+       (g_conv_algo == 2 && ((tn == 2 && nr == 4) || (tn == 4 && nr == 8))))) {
     d.tn = tn;
     d.nr = nr;
     d.nblk = 1;
@@ -1435,6 +1476,11 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   //  do not depend on the remainder switch or the grouped path)
   if (yd->h < 8 || ad->n * ceil_div(yd->h, 8) * d.tiles_w * t.nblk < 768) d.tm = 2;
   d.tiles_h = (int)ceil_div(yd->h, 2 * d.tm);
+  // the remainder form has one N block: only where the tiles alone fill the chip twice
+  // (algo 2 forces it wherever legal, for the tests)
+  if (d.nr && g_conv_algo != 2 && ad->n * d.tiles_h * d.tiles_w < 512) {
+    d.tn = t.tn; d.nblk = t.nblk; d.nr = 0;
+  }
   return d;
 }
 
@@ -1448,6 +1494,11 @@ static bool dconv_use(const vae2_act* ad, const vae2_act* yd, int k, int stride,
   return ad->w >= 16 && ad->n * d.tiles_h * d.tiles_w * d.nblk >= 256;
 }
 
+int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                 const float* bias, float* y, const vae2_act* yd, float beta,
+                 float* stats, bool flip, hipStream_t s, const char* fn);
+
+#if VAE2_PART(2)
 template <int TM, bool FLIP>
 static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s,
                             int nr = 0) {
@@ -1468,6 +1519,8 @@ static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipSt
   }
 }
 
+#endif  // VAE2_PART(2)
+
 static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, const float* wp,
                         uint32_t w_bytes, const float* bias, float* y, const vae2_act* yd,
                         float beta, float* stats) {
@@ -1482,10 +1535,11 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
 }
 
 static size_t dconv_shm(const DTile& d) {
-  return ((size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) + (size_t)d.nr * 9 * d.cs4 * 4) *
-         sizeof(float);
+  return ((size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) +
+          (size_t)d.nr * ((9 * d.cs4 + 7) / 8) * 32) * sizeof(float);
 }
 
+#if VAE2_PART(2)
 template <int TM, bool FLIP>
 static void dconv_group_launch_tn(const DConvGroup& g, int tn, dim3 grid, size_t shm,
                                   hipStream_t s) {
@@ -1500,9 +1554,9 @@ static void dconv_group_launch_tn(const DConvGroup& g, int tn, dim3 grid, size_t
   }
 }
 
-static int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
-                        const float* bias, float* y, const vae2_act* yd, float beta,
-                        float* stats, bool flip, hipStream_t s, const char* fn) {
+int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                 const float* bias, float* y, const vae2_act* yd, float beta,
+                 float* stats, bool flip, hipStream_t s, const char* fn) {
   DTile d = pick_dtile(ad, yd);
   DConv p{};
   p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
@@ -1522,6 +1576,8 @@ static int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uin
   }
   return check_launch(fn);
 }
+
+#endif  // VAE2_PART(2)
 
 static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
   DTile d = pick_dtile(ad, yd);
@@ -1586,6 +1642,7 @@ static size_t wgrad3_lds(const W3Tile& t) {
   return ((size_t)16 * t.tm * (npx + 4) + (size_t)(t.csw + 1) * lpx) * sizeof(float);
 }
 
+#if VAE2_PART(3)
 template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
                              hipStream_t s) {
@@ -1622,9 +1679,11 @@ static void wgrad3_launch(const WGrad3& p, const W3Tile& t, dim3 grid, size_t sh
   if (t.pf) wgrad3_launch_tm<BH, true>(p, t, grid, shm, s);
   else wgrad3_launch_tm<BH, false>(p, t, grid, shm, s);
 }
+#endif  // VAE2_PART(3)
 
 extern "C" {
 
+#if VAE2_PART(0)
 int64_t vae2_conv2d_packed_size(int64_t cout, int64_t cin, int k, int mode) {
   int rows = mode == 0 ? round_up((int)cout, 64) : round_up((int)cin, 64);
   int cols4 = mode == 0 ? round_up((int)cin, 4) : round_up((int)cout, 4);
@@ -1662,6 +1721,9 @@ int vae2_conv2d_set_mfma_bf16(int on) {
   return prev;
 }
 
+#endif  // VAE2_PART(0)
+
+#if VAE2_PART(3)
 int vae2_wgrad_defer(int on) {
   const int prev = g_wr_defer ? 1 : 0;
   g_wr_defer = on != 0;
@@ -1693,6 +1755,9 @@ int vae2_wgrad_flush(void* stream) {
   return 0;
 }
 
+#endif  // VAE2_PART(3)
+
+#if VAE2_PART(0)
 int vae2_conv2d_set_algo(int algo) {
   const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) + (g_dconv_nr ? 0 : 16);
   const int a = algo & 7;
@@ -1822,6 +1887,9 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
   return launch_igemm(p, 1, as_stream(stream), fn, ncls);
 }
 
+#endif  // VAE2_PART(0)
+
+#if VAE2_PART(2)
 // Independent convolutions in one call (one HRNet depth level): the jobs the direct 3x3
 // kernel takes are launched together, up to kDcGroup per launch, grouped by tile shape
 // and direction (jobs writing the same output never share a launch); the others go
@@ -1879,7 +1947,8 @@ int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
     bool direct = g_conv_group && J.x && J.wp && J.y &&
                   (fwd ? conv_shapes_ok(ad, od, J.k, J.stride, J.pad)
                        : conv_shapes_ok(od, ad, J.k, J.stride, J.pad)) &&
-                  fits32(ad) && fits32(od) && dconv_use(ad, od, J.k, J.stride, J.pad, J.x);
+                  fits32(ad) && fits32(od) && dconv_use(ad, od, J.k, J.stride, J.pad, J.x) &&
+                  pick_dtile(ad, od).nr == 0;  // (remainder layers: their own launch)
     if (!direct) {
       int rc = fwd ? vae2_conv2d_fwd(J.x, ad, J.wp, J.bias, J.y, od, J.k, J.stride, J.pad,
                                      J.beta, J.stats, stream)
@@ -1922,6 +1991,9 @@ int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
   return 0;
 }
 
+#endif  // VAE2_PART(2)
+
+#if VAE2_PART(3)
 int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, int k) {
   if (!act_ok(xd) || !act_ok(dyd)) return 0;
   int ncol4 = k * k * round_up((int)xd->c, 4);
@@ -2033,5 +2105,6 @@ int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,
   return vae2_conv2d_bwd_weight_ld(x, xd, dy, dyd, dw, xd->c * k * k, dbias, k, stride, pad,
                                    accumulate, ws, ws_size, stream);
 }
+#endif  // VAE2_PART(3)
 
 }  // extern "C"
