@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--clip-length", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=None,
+                    help="clips per CPU step (default: the GPU's clips per step)")
+    ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--profile-json", default=None,
@@ -80,6 +81,10 @@ def parse():
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
+    ap.add_argument("--full-step", action="store_true",
+                    help="the reference's full training iteration (function.py:443-512): "
+                         "GAN_LAMBDA 1 (both LSGAN generator terms through the two "
+                         "discriminators) + the discriminator step with its own Adam")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto: at N=1).  The "
                          "eager step measured 0-3%% faster on an idle host but 10-20%% "
@@ -98,6 +103,8 @@ def load_config(args):
     if args.height is not None or args.width is not None:
         w, h = config.TRAIN.IMAGE_SIZE
         opts += ["TRAIN.IMAGE_SIZE", f"[{args.width or w}, {args.height or h}]"]
+    if args.full_step:
+        opts += ["TRAIN.GAN_LAMBDA", "1.0", "MI355X.ELBO_ONLY", "False"]
     if args.clip_length is not None:  # 3 segments of L frames
         opts += ["TRAIN.CLIP_LENGTH", str(args.clip_length),
                  "DATASET.NUM_CLASSES", str(args.clip_length)]
@@ -106,13 +113,16 @@ def load_config(args):
     return config
 
 
-def build_models(config):
+def build_models(config, with_d=False):
     """train.py's construction order (train.py:79-82) through the lib/ factories."""
     import models
     torch.manual_seed(0)
     ed = models.enc_hrnet.get_encdec_model(config)
     ez = models.enc_hrnet.get_encz_model(config)
-    return ed, ez
+    if not with_d:
+        return ed, ez
+    return (ed, ez, models.enc_hrnet.get_D_sequence_model(config),
+            models.enc_hrnet.get_D_frame_model(config))
 
 
 def pmc_traffic(kernel):
@@ -168,7 +178,7 @@ def cpu_baseline(args, config, gpu_batch):
     torch.set_num_threads(cores)
     L = config.TRAIN.CLIP_LENGTH
     W, H = config.TRAIN.IMAGE_SIZE
-    B = args.cpu_batch
+    B = args.cpu_batch or gpu_batch
     ed, ez = build_models(config)
     params = list(ez.parameters()) + list(ed.parameters())
     opt = torch.optim.Adam(params, lr=config.TRAIN.LR)
@@ -183,7 +193,8 @@ def cpu_baseline(args, config, gpu_batch):
         terms["loss_all"].backward()
         opt.step()
 
-    step()  # warm-up
+    if args.cpu_steps > 1:
+        step()  # warm-up (the default single timed step has none: ~20 s at 8 clips)
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
         step()
@@ -192,10 +203,11 @@ def cpu_baseline(args, config, gpu_batch):
             "kind": "port",
             "sample": f"oracle/ref_cpu.py ELBO step fwd+bwd+torch Adam (the reference's ATen "
                       f"ops), HRNet-W18-small-v2 {H}x{W}, {B} clips x {3 * L} frames per step "
-                      f"(the GPU runs {gpu_batch} clips/step; frames/s is per-frame, so the "
-                      f"sample size only bounds the run time), fp32, 1 warm-up + "
-                      f"{args.cpu_steps} timed steps ({dt:.2f} s/step), torch threads={cores} "
-                      f"of {aff} in the affinity mask, CPU: {cpu_model()}"}
+                      f"(the GPU runs {gpu_batch} clips/step), fp32, "
+                      f"{'1 warm-up + ' if args.cpu_steps > 1 else ''}{args.cpu_steps} timed "
+                      f"step(s) ({dt:.2f} s/step), torch threads={cores} = the box's CPU "
+                      f"share for one GPU (OMP_NUM_THREADS; {aff} in the affinity mask), "
+                      f"CPU: {cpu_model()}"}
 
 
 def main():
@@ -209,8 +221,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from core.criterion import KLLoss, L1Loss
-    from utils.utils import FullModel_encdec
+    from core.criterion import KLLoss, L1Loss, lsgan_adversarial_loss
+    from utils.utils import FullModel_D, FullModel_encdec
     from vae2 import dist as vdist
     from vae2 import prof
     from vae2.optim import FusedAdam
@@ -230,16 +242,27 @@ def main():
     L = config.TRAIN.CLIP_LENGTH
     W, H = config.TRAIN.IMAGE_SIZE
     B = config.TRAIN.BATCH_SIZE_PER_GPU
-    ed, ez = build_models(config)
-    fm = FullModel_encdec(ez, ed, None, None, L1Loss(), KLLoss(), None,
+    full = args.full_step
+    if full:
+        ed, ez, dseq, dfrm = build_models(config, with_d=True)
+    else:
+        (ed, ez), dseq, dfrm = build_models(config), None, None
+    fm = FullModel_encdec(ez, ed, dseq, dfrm, L1Loss(), KLLoss(),
+                          lsgan_adversarial_loss() if full else None,
                           config.TRAIN.X1RECON_LAMBDA, config.TRAIN.X2RECON_LAMBDA,
                           config.TRAIN.X3RECON_LAMBDA, config.TRAIN.GAN_LAMBDA).to(dev)
     fm.train()
     fm.defer_checks = True
     opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=config.TRAIN.LR)
+    fmd = opt_d = None
+    if full:  # function.py:503-512: D on real x2t vs the detached x2t_hat, its own Adam
+        fmd = FullModel_D(dseq, dfrm, lsgan_adversarial_loss()).to(dev)
+        fmd.train()
+        opt_d = FusedAdam([dseq, dfrm], lr=config.TRAIN.LR)
     if world > 1:
-        for f in opt.flats:
-            dist.broadcast(f.data, src=0)
+        for o in (opt, opt_d):
+            for f in (o.flats if o is not None else []):
+                dist.broadcast(f.data, src=0)
     g = torch.Generator().manual_seed(1 + rank)
     xs = [torch.randn(B, 3 * L, H, W, generator=g).to(dev) for _ in range(3)]
     zc = ez.z_dim
@@ -247,10 +270,16 @@ def main():
     def eager_step():
         opt.zero_grad()
         fm.set_noise(torch.randn(B, zc, 1, 1, device=dev), torch.randn(B, zc, 1, 1, device=dev))
-        losses = fm(*xs, 1.0)[0]
+        losses, _, x2p, _ = fm(*xs, 1.0)
         losses[0].backward()
         vdist.allreduce_grads(opt.flats)
         opt.step()
+        if fmd is not None:
+            opt_d.zero_grad()
+            ld = fmd(xs[1], x2p.detach())[0]
+            ld.backward()
+            vdist.allreduce_grads(opt_d.flats)
+            opt_d.step()
         return losses[0]
 
     use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
@@ -304,9 +333,12 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (Gaussian Cityscapes-shaped clips resident in HBM; random-init "
                     "weights, reference init seed 0)",
-            "config": {"workload": f"VAE2 ELBO step (encz + encoder + 2 decoders fwd/bwd + "
-                                   f"Adam), HRNet-W18-small-v2, {H}x{W}, {B} clips/GPU x "
-                                   f"{3 * L} frames (CLIP_LENGTH={L})",
+            "config": {"workload": (f"VAE2 full training iteration (ELBO + GAN_LAMBDA 1 "
+                                    f"LSGAN terms through both discriminators, Adam; then the "
+                                    f"discriminator step, its Adam)" if full else
+                                    f"VAE2 ELBO step (encz + encoder + 2 decoders fwd/bwd + "
+                                    f"Adam)") + f", HRNet-W18-small-v2, {H}x{W}, {B} clips/GPU "
+                                   f"x {3 * L} frames (CLIP_LENGTH={L})",
                        "yaml": os.path.relpath(args.cfg, ROOT),
                        "global_batch": world * B, "frames_per_clip": 3 * L,
                        "image": [H, W], "parallelism": f"dp{world}",
@@ -329,7 +361,7 @@ def main():
             roof["traffic_unit"] = "HBM bytes/launch (PMC, profiles/)"
             roof["step_frac"] = round(conv_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["step_gflop"] = round(conv_gf, 1)
-            if ref_gf is not None and L == 3:
+            if ref_gf is not None and L == 3 and not full:
                 # the noted conv + head FLOPs must equal the reference's FlopCounter total
                 # less what the commuted heads legitimately skip (tests assert "reconciled")
                 skip = B * head_skip_gflop_per_clip(ed, H, W)
@@ -342,7 +374,7 @@ def main():
                     "ratio": round(conv_gf / want, 4),
                     "reconciled": abs(conv_gf / want - 1.0) < 0.01,
                     "note_conflicts": summ["note_conflicts"]}
-            if ref_gf is not None and L == 3:
+            if ref_gf is not None and L == 3 and not full:
                 roof["step_frac_ref_flops"] = round(
                     B * ref_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["measured"] = (f"{n} eager steps after the timed region, every C-ABI call "
@@ -354,7 +386,7 @@ def main():
             if args.profile_json:
                 with open(args.profile_json, "w") as f:
                     json.dump(summ, f, indent=1)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not full:
             out["cpu_baseline"] = cpu_baseline(args, config, B)
         print(json.dumps(out), flush=True)
     if world > 1:

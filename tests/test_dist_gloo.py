@@ -106,3 +106,19 @@ def test_two_ranks_equal_one_rank_with_sync_bn():
         assert abs(loss - float(g["loss_loss_all"])) <= 1e-5 * abs(float(g["loss_loss_all"]))
     for rank, _, preds in res:
         np.testing.assert_allclose(preds[1], g["x2p"][rank], rtol=0, atol=1e-4 * np.abs(g["x2p"]).max())
+
+
+def test_decoder_tail_range_is_the_decoders():
+    """The early gradient buckets (vae2.dist.early_reduce_hook) cover exactly the
+    trailing decf_* / decp_* parameters of the encoder-decoder's flat buffer."""
+    from helpers import build, make_cfg
+    from vae2 import dist as vdist
+    from vae2.params import flatten
+    ed, _ = build(make_cfg("tiny"))
+    flat = flatten(ed)
+    start = vdist.tail_range(flat)
+    assert start is not None and 0 < start < flat.numel
+    names = [n for n, o in zip(flat.names, flat.offsets) if o >= start]
+    assert names and all(n.startswith(("decf_", "decp_")) for n in names)
+    assert not any(n.startswith(("decf_", "decp_")) for n, o in zip(flat.names, flat.offsets)
+                   if o < start)

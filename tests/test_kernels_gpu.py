@@ -718,7 +718,7 @@ def test_conv2d_multi_grouped_equals_single_calls():
     from vae2 import _lib, ops
     from vae2._lib import Act
     lib = _lib.load()
-    prev = lib.vae2_conv2d_set_algo(2)
+    prev = lib.vae2_conv2d_set_algo(2 + 16)  # (VALU-remainder layers are never grouped)
     prev_g = lib.vae2_conv2d_set_grouping(1)
     s = ops.stream_ptr()
     torch.manual_seed(5)

@@ -9,7 +9,14 @@ One process per GPU; the "nccl" backend of PyTorch-ROCm is RCCL over xGMI.
   global exactly as with SyncBatchNorm; parameter gradients use local sums and
   are averaged by the gradient all-reduce, as DDP does.
 * Gradients: the flat gradient buffer of each model is all-reduced (sum) in
-  buckets and scaled by 1/world in a HIP kernel (DDP's mean).
+  buckets and scaled by 1/world in a HIP kernel (DDP's mean).  The decoders' range
+  of the encoder-decoder buffer (its tail: decf_* / decp_* parameters) is final as
+  soon as the gradient of the encoder output x2t_hat is (every decoder node feeds
+  it), so a hook on that tensor starts its buckets then, on a communicator of their
+  own, while the encoder and posterior backward still run (DDP's bucket overlap
+  without per-parameter hooks: the HIP kernels accumulate into the flat buffer).
+  SyncBN exchanges stay on the default communicator, so they never queue behind a
+  gradient bucket.
 """
 import os
 
@@ -21,10 +28,15 @@ from ._lib import call
 
 _SYNC_BN_GROUP = None
 _SYNC_BN = False
+_GRAD_GROUP = None
+_EARLY = {}       # id(flat) -> (flat, end offset already launched, [async works])
+FORCE = False     # the distributed code path at world size 1 (tests: bit-identity)
+OVERLAP = True    # early decoder buckets (A/B: off = everything after backward)
 
 
 def is_dist():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return (dist.is_available() and dist.is_initialized() and
+            (dist.get_world_size() > 1 or FORCE))
 
 
 def world_size():
@@ -81,15 +93,63 @@ def bucket_allreduce(buf, bucket_elems=BUCKET_ELEMS, group=None):
         all_reduce_(buf[off:off + bucket_elems], group=group)
 
 
+def grad_group():
+    """The gradient buckets' communicator (created once, collectively, on first use)."""
+    global _GRAD_GROUP
+    if _GRAD_GROUP is None:
+        _GRAD_GROUP = dist.new_group(backend=dist.get_backend())
+    return _GRAD_GROUP
+
+
+def tail_range(flat, prefixes=("decf_", "decp_")):
+    """First offset of the trailing parameters whose names start with `prefixes`
+    (None unless every parameter from there on does)."""
+    idx = [i for i, n in enumerate(flat.names) if n.startswith(prefixes)]
+    if not idx or idx != list(range(idx[0], len(flat.names))):
+        return None
+    return flat.offsets[idx[0]]
+
+
+def early_reduce_hook(t, flat, start):
+    """Start the all-reduce of flat.grad[start:] when t's gradient is complete."""
+    if not (OVERLAP and is_dist() and t.requires_grad and start is not None):
+        return
+    if dist.get_backend(grad_group()) == "gloo":
+        return  # host-staged gloo reduces synchronously: nothing to overlap
+
+    def hook(g):
+        streams.join_all()  # the decoders' side-stream work (and its deferred reductions)
+        buf = flat.grad
+        works = [dist.all_reduce(buf[off:off + BUCKET_ELEMS], group=grad_group(),
+                                 async_op=True)
+                 for off in range(start, buf.numel(), BUCKET_ELEMS)]
+        _EARLY[id(flat)] = (start, works)
+        return g
+
+    t.register_hook(hook)
+
+
 def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
     """Mean-reduce the flat gradient buffers over all ranks (DDP semantics)."""
     if not is_dist():
         return
     streams.join_all()
     ws = world_size()
+    pending = []
     for f in flats:
         g = f.grad
-        bucket_allreduce(g, bucket_elems)
+        start, works = _EARLY.pop(id(f), (g.numel(), []))
+        head = g[:start]
+        if dist.get_backend(grad_group()) == "gloo":
+            bucket_allreduce(head, bucket_elems, group=grad_group())
+        else:
+            works = [dist.all_reduce(head[off:off + bucket_elems], group=grad_group(),
+                                     async_op=True)
+                     for off in range(0, head.numel(), bucket_elems)] + works
+        pending.append((g, works))
+    for g, works in pending:
+        for w in works:
+            w.wait()  # the compute stream waits for the bucket (no host sync)
         call("vae2_scale", ops.ptr(g), ops.ptr(g), g.numel(), 1.0 / ws, ops.stream_ptr())
 
 

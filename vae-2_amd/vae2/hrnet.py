@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import heads as vheads
+from . import dist as vdist
 from . import ops, streams
 
 BN_MOMENTUM = 0.01
@@ -520,6 +521,11 @@ class HighResolutionNetED(HighResolutionNet):
         """Encoder then both decoders; the past decoder runs on a side stream
         concurrently with the future decoder (they are independent)."""
         x2t = self.encode(x, z, code, trunk)
+        flat = getattr(self, "_vae2_flat", None)
+        if flat is not None and not is_baseline:  # the decoders' gradient buckets start early
+            if not hasattr(self, "_dec_start"):
+                self._dec_start = vdist.tail_range(flat)
+            vdist.early_reduce_hook(x2t, flat, self._dec_start)
         with torch.no_grad() if is_baseline else contextlib.nullcontext():
             with streams.on_side(1, inputs=[x2t, z]) as sp:
                 x1t = self.decode("decp_", x2t, z)
