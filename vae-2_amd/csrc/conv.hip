@@ -405,6 +405,10 @@ struct DConv {
 
 constexpr int kDcBW = 32;     // tile columns
 constexpr int kDcMaxCs4 = 8;  // quads per slab
+// (A offset, weight offset) of every K step of a slab (chunks of 4 (tap, quad) steps, an
+// even number of chunks, + the 2 chunks the loop prefetches past the end), in LDS after
+// the tile and the remainder weights
+constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 8;
 
 // One output tile: bm = tile index (image-major), by = N block, nrows = tiles of the
 // layer (rows of its BN partial statistics).
@@ -475,6 +479,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   // floats per remainder channel in rw: the K steps of an even number of chunks (the main
   // loop runs chunks in pairs), zero past the slab's 9 x qs steps
   const int rws = ((9 * p.cs4 + 7) >> 3) * 32;
+  int2* const tab = reinterpret_cast<int2*>(rw + NR * rws);
   float racc[NRL > 0 ? NRL : 1];
 #pragma unroll
   for (int j = 0; j < NRL; ++j) racc[j] = 0.f;
@@ -484,6 +489,19 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const int qs = Q - q0 < p.cs4 ? Q - q0 : p.cs4;
     // ---- stage the halo tile of this slab (zero outside the image / past a_c) ----
     __syncthreads();
+    const int nch = (9 * qs + 3) >> 2;
+    {  // the slab's K-step table: entry k = (tap, quad) step k of the chunk sequence
+      const int k = threadIdx.x;
+      if (k < ((nch + 1) >> 1) * 8 + 8) {  // (steps past the 9 taps: zero weights)
+        const int t = k / qs, q = k - t * qs;
+        const bool tv = t < 9;
+        const int tt = tv ? t : 0;
+        const int dh = tt / 3 - 1, dw = tt - 3 * (tt / 3) - 1;
+        const int tl = FLIP ? 8 - tt : tt;
+        tab[k] = make_int2((dh * LW + dw) * csp + 4 * q,
+                           tv ? (int)((uint32_t)(tl * p.a_c4 + (q0 + q) * 4) * 4u) : (int)kOOB);
+      }
+    }
     if constexpr (NR > 0) {  // remainder weights of the slab [j][(tap, quad)][4], FLIP
       const int per = ((9 * qs + 7) >> 3) * 32;  // whole chunk pairs: zero tail
       for (int i = threadIdx.x; i < NR * per; i += 256) {
@@ -532,51 +550,37 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     }
     __syncthreads();
     // ---- 9 taps x qs quads of K from LDS ----
-    const int nch = (9 * qs + 3) >> 2;
-    // (tap, quad) of this lane group's next K chunk: q advances by 4 quads per chunk;
-    // the carry into the tap is at most 4 (qs >= 1), taken branch-free
-    int t = (g >= qs) + (g >= 2 * qs) + (g >= 3 * qs), q = g - t * qs;
-    auto step = [&]() {
-      const int nq = q + 4;
-      const int dt = (nq >= qs) + (nq >= 2 * qs) + (nq >= 3 * qs) + (nq >= 4 * qs);
-      q = nq - dt * qs;
-      t += dt;
-    };
+    // chunk c, lane group g: K step 4c + g, its A / weight offsets from the table
+    int kc = g;
     auto load = [&](f4* fa, f4* fb) {
-      const bool tv = t < 9;
-      const int tt = tv ? t : 0;
-      const int dh = (tt >= 3) + (tt >= 6) - 1;
-      const int dw = tt - 3 * (dh + 1) - 1;
-      const int aoff = (dh * LW + dw) * csp + 4 * q;
+      const int2 e = tab[kc];
+      kc += 4;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const f4*>(&tile[abase[i] + aoff]);
-      const int tl = FLIP ? 8 - tt : tt;
-      const uint32_t woff = tv ? (uint32_t)(tl * p.a_c4 + (q0 + q) * 4) * 4u : kOOB;
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const f4*>(&tile[abase[i] + e.x]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
-      step();
+      for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + (uint32_t)e.y);
     };
-    // the remainder's share of a chunk: its 4 (tap, quad) K steps, wave-uniform counters,
-    // branch-free (steps past the 9 taps read tap 8 against the zeroed tail of rw)
-    int rkq = 0, rt = 0, rq = 0;
+    // the remainder's share of a chunk: its 4 K steps, A offsets from the same table
+    // (wave-uniform; steps past the 9 taps read tap 0 against the zeroed tail of rw)
+    int rkq = 0;
     auto rem = [&]() {
       if constexpr (NR > 0) {
+        const int4 o4 = reinterpret_cast<const int4*>(tab)[rkq >> 1];
+        const int4 o5 = reinterpret_cast<const int4*>(tab)[(rkq >> 1) + 1];
+        const int xo[4] = {o4.x, o4.z, o5.x, o5.z};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int tc = rt < 9 ? rt : 8;
-          const int dh = (tc >= 3) + (tc >= 6) - 1, dw = tc - 3 * (dh + 1) - 1;
-          const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + (dh * LW + dw) * csp + 4 * rq]);
+          const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + xo[u]]);
 #pragma unroll
           for (int j = 0; j < NRL; ++j) {
-            const f4 wv = *reinterpret_cast<const f4*>(&rw[(rh * NRL + j) * rws + 4 * rkq]);
+            const f4 wv = *reinterpret_cast<const f4*>(&rw[(rh * NRL + j) * rws + 4 * (rkq + u)]);
             racc[j] = __builtin_fmaf(xv[0], wv[0], racc[j]);
             racc[j] = __builtin_fmaf(xv[1], wv[1], racc[j]);
             racc[j] = __builtin_fmaf(xv[2], wv[2], racc[j]);
             racc[j] = __builtin_fmaf(xv[3], wv[3], racc[j]);
           }
-          ++rkq;
-          if (++rq == qs) { rq = 0; ++rt; }
         }
+        rkq += 4;
       }
     };
     if (!BF) {
@@ -1536,7 +1540,7 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
 
 static size_t dconv_shm(const DTile& d) {
   return ((size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) +
-          (size_t)d.nr * ((9 * d.cs4 + 7) / 8) * 32) * sizeof(float);
+          (size_t)d.nr * ((9 * d.cs4 + 7) / 8) * 32 + 2 * kDcTab) * sizeof(float);
 }
 
 #if VAE2_PART(2)
