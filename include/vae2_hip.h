@@ -67,12 +67,13 @@ int vae2_conv2d_set_algo(int algo);
  * rounded to bf16 (RNE) as they enter the MFMA; accumulation, storage, BatchNorm and the
  * optimizer stay fp32).  Returns the previous setting.  Process-wide.             */
 int vae2_conv2d_set_mfma_bf16(int on);
-/* Deferred weight-gradient reductions (per calling thread): while on, every
+/* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
- * reduction; vae2_wgrad_flush launches the queued reductions together (up to 8 per
- * launch, in queue order, each on the stream its weight gradient was issued on).  The
- * caller keeps each call's workspace alive until the flush is enqueued and does not
- * queue two reductions into the same dW elements.  Returns the previous setting.   */
+ * reduction (one process-wide queue); vae2_wgrad_flush launches the queued reductions
+ * together on `stream` (up to 32 per launch, in queue order; reductions into the same
+ * dW elements go to successive launches).  The caller orders `stream` after the
+ * streams the weight gradients were issued on and keeps each call's workspace alive
+ * until the flush is enqueued.  Returns the previous setting.                        */
 int vae2_wgrad_defer(int on);
 int vae2_wgrad_flush(void* stream);
 

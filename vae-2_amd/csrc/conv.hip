@@ -21,6 +21,7 @@
 //
 // Replaces nn.Conv2d forward/backward for every conv of enc_hrnet.py (call sites
 // in include/vae2_hip.h).
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -1311,7 +1312,7 @@ struct WRJob {
   int64_t ld;
   int splits, cout, cin, cin4, k, accumulate, blk0;
 };
-constexpr int kWrMaxJobs = 8;
+constexpr int kWrMaxJobs = 32;  // (kernel argument: 32 x 56 B)
 struct WRMulti {
   WRJob j[kWrMaxJobs];
   int n;
@@ -1356,8 +1357,11 @@ struct WRQueued {
   WRJob job;
   hipStream_t stream;
 };
+// the deferral switch is per thread (set inside the calling thread's backward functions);
+// the queue is shared, so the end-of-backward flush may run on any thread
 static thread_local bool g_wr_defer = false;
-static thread_local std::vector<WRQueued> g_wr_queue;
+static std::vector<WRQueued> g_wr_queue;
+static std::mutex g_wr_mu;
 
 struct WTile {
   int tm, tn, gx, gy, splits, px_split;
@@ -1738,14 +1742,30 @@ int vae2_wgrad_flush(void* stream) {
   const char* fn = "vae2_wgrad_flush";
   hipStream_t want = as_stream(stream);
   std::vector<WRQueued> q;
-  q.swap(g_wr_queue);
+  {
+    std::lock_guard<std::mutex> lk(g_wr_mu);
+    q.swap(g_wr_queue);
+  }
   size_t i = 0;
-  while (i < q.size()) {  // consecutive jobs of one stream, kWrMaxJobs per launch
+  // every job on the given stream: the caller orders it after the jobs' own streams
+  while (i < q.size()) {  // kWrMaxJobs per launch
     WRMulti m{};
-    hipStream_t st = q[i].stream;
+    hipStream_t st = want;
     int blocks = 0;
-    while (i < q.size() && m.n < kWrMaxJobs && q[i].stream == st) {
+    while (i < q.size() && m.n < kWrMaxJobs) {
       WRJob j = q[i].job;
+      // a job accumulating into dW elements a job of this launch writes waits for the
+      // next launch (e.g. a discriminator applied to real and fake inputs)
+      const float* lo = j.dw;
+      const float* hi = j.dw + (int64_t)(j.cout - 1) * j.ld + (int64_t)j.cin * j.k * j.k;
+      bool clash = false;
+      for (int u = 0; u < m.n; ++u) {
+        const float* lo2 = m.j[u].dw;
+        const float* hi2 = m.j[u].dw + (int64_t)(m.j[u].cout - 1) * m.j[u].ld +
+                           (int64_t)m.j[u].cin * m.j[u].k * m.j[u].k;
+        if (lo < hi2 && lo2 < hi) clash = true;
+      }
+      if (clash) break;
       j.blk0 = blocks;
       blocks += (int)ceil_div((int64_t)j.cout * j.k * j.k * j.cin4, 32);
       m.j[m.n++] = j;
@@ -1755,7 +1775,6 @@ int vae2_wgrad_flush(void* stream) {
     const int rc = check_launch(fn);
     if (rc) return rc;
   }
-  (void)want;
   return 0;
 }
 
@@ -2079,6 +2098,7 @@ reduce:
   int rc = 0;
   if (g_wr_defer) {
     WRJob j{ws, dw, dw_ld, splits, (int)dyd->c, (int)xd->c, cin4, k, accumulate, 0};
+    std::lock_guard<std::mutex> lk(g_wr_mu);
     g_wr_queue.push_back(WRQueued{j, s});
   } else {
     VAE2_LAUNCH(wgrad_reduce_kernel, dim3((unsigned)ceil_div(slab, 32)), dim3(256), 0, s,

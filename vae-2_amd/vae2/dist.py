@@ -118,7 +118,8 @@ def early_reduce_hook(t, flat, start):
         return  # host-staged gloo reduces synchronously: nothing to overlap
 
     def hook(g):
-        streams.join_all()  # the decoders' side-stream work (and its deferred reductions)
+        ops.flush_wgrad()   # the decoders' queued weight-gradient reductions
+        streams.join_all()  # the decoders' side-stream work
         buf = flat.grad
         works = [dist.all_reduce(buf[off:off + BUCKET_ELEMS], group=grad_group(),
                                  async_op=True)

@@ -29,7 +29,7 @@ import ctypes
 import torch
 import torch.distributed as dist
 
-from . import _lib, prof
+from . import _lib, prof, streams
 from ._lib import Act, call
 
 _F32 = torch.float32
@@ -356,12 +356,36 @@ def _conv_fwd_queued(group, x, weight, bias, spec, stats):
 
 _WGRAD_BATCH = [0]  # open wgrad_batch contexts
 _WS_HOLD = []       # workspaces of queued weight-gradient reductions
+_WGRAD_CB = [False]  # an end-of-backward flush is queued with the autograd engine
+
+
+def flush_wgrad():
+    """Launch every queued weight-gradient reduction on the current stream, after the
+    side streams' work (the convs that wrote the partial slabs), and release the held
+    workspaces (recorded on this stream, so the allocator reuses them only after it)."""
+    streams.join_all()
+    cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+    try:
+        call("vae2_wgrad_flush", stream_ptr())
+    finally:
+        if cur is not None:
+            for t_ in _WS_HOLD:
+                if t_.is_cuda:
+                    t_.record_stream(cur)
+        _WS_HOLD.clear()
+
+
+def _end_of_backward():
+    _WGRAD_CB[0] = False
+    flush_wgrad()
 
 
 class wgrad_batch:
-    """Context: the weight-gradient slab reductions of the convs in it share launches
-    (vae2_wgrad_defer / vae2_wgrad_flush, up to 8 per launch); their workspaces are held
-    until the flush is enqueued (stream order then frees them safely)."""
+    """Context: the weight-gradient slab reductions of the convs in it are queued
+    (vae2_wgrad_defer) and launched together, up to 32 per launch, once at the end of
+    the backward pass (an autograd engine final callback; the early gradient buckets of
+    vae2.dist flush first), or at the context's exit outside a backward.  Their
+    workspaces are held until then."""
 
     def __enter__(self):
         _lib.load().vae2_wgrad_defer(1)
@@ -371,11 +395,13 @@ class wgrad_batch:
     def __exit__(self, *exc):
         _WGRAD_BATCH[0] -= 1
         if _WGRAD_BATCH[0] == 0:
-            try:
-                call("vae2_wgrad_flush", stream_ptr())
-            finally:
-                _lib.load().vae2_wgrad_defer(0)
-                _WS_HOLD.clear()
+            _lib.load().vae2_wgrad_defer(0)
+            if not _WGRAD_CB[0]:
+                try:
+                    torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+                    _WGRAD_CB[0] = True
+                except RuntimeError:  # not inside a backward pass: flush now
+                    flush_wgrad()
         return False
 
 
