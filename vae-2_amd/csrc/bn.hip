@@ -294,6 +294,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q_kernel(
   }
 }
 
+// Thread tid's share of a per-channel reduction over partial rows (rows tid, tid+256,
+// ... of column c; with `two`, also of the second block of rows): 4 rows' loads issued
+// before their adds (latency, not bandwidth, bounds these small reductions), the adds
+// in the same order as a plain strided loop, so the result is bit for bit the same.
+__device__ __forceinline__ void rows_sum2(const float* __restrict__ part, int64_t rows,
+                                          int64_t C, int c, int tid, double& a, double& b,
+                                          bool two = true) {
+  constexpr int U = 8;
+  for (int64_t r0 = tid; r0 < rows; r0 += 256 * U) {
+    float x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + 256 * u;
+      x[u] = r < rows ? part[r * C + c] : 0.f;
+      y[u] = (two && r < rows) ? part[(rows + r) * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r0 + 256 * u < rows) {
+        a += (double)x[u];
+        b += (double)y[u];
+      }
+    }
+  }
+}
+
 // One block per channel: sums[q][c] (+)= sum_rows part[q][row][c] in double.
 __global__ __launch_bounds__(256) void partials_reduce_kernel(
     const float* __restrict__ part, int64_t rows, int64_t C, double* sums,
@@ -302,10 +328,7 @@ __global__ __launch_bounds__(256) void partials_reduce_kernel(
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   double a = 0.0, b = 0.0;
-  for (int64_t r = tid; r < rows; r += 256) {
-    a += (double)part[r * C + c];
-    b += (double)part[(rows + r) * C + c];
-  }
+  rows_sum2(part, rows, C, c, tid, a, b);
   a = wave_sum_d(a);
   b = wave_sum_d(b);
   if ((tid & 63) == 0) {
@@ -342,10 +365,7 @@ __global__ __launch_bounds__(256) void reduce_then_kernel(
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   double a = 0.0, b = 0.0;
-  for (int64_t r = tid; r < rows; r += 256) {
-    a += (double)part[r * C + c];
-    b += (double)part[(rows + r) * C + c];
-  }
+  rows_sum2(part, rows, C, c, tid, a, b);
   a = wave_sum_d(a);
   b = wave_sum_d(b);
   if ((tid & 63) == 0) {
@@ -514,7 +534,10 @@ __global__ __launch_bounds__(256) void colsum_to_float_kernel(
   __shared__ double red[4];
   const int c = blockIdx.x, tid = threadIdx.x;
   double a = 0.0;
-  for (int64_t r = tid; r < rows; r += 256) a += (double)part[r * C + c];
+  {
+    double b = 0.0;
+    rows_sum2(part, rows, C, c, tid, a, b, false);
+  }
   a = wave_sum_d(a);
   if ((tid & 63) == 0) red[tid >> 6] = a;
   __syncthreads();
@@ -774,10 +797,7 @@ __global__ __launch_bounds__(256) void reduce_then_multi_kernel(FinMulti m) {
   const int c = blockIdx.x - L.blk0;
   const int tid = threadIdx.x;
   double a = 0.0, b = 0.0;
-  for (int64_t r = tid; r < L.rows; r += 256) {
-    a += (double)L.part[r * L.C + c];
-    b += (double)L.part[(L.rows + r) * L.C + c];
-  }
+  rows_sum2(L.part, L.rows, L.C, c, tid, a, b);
   a = wave_sum_d(a);
   b = wave_sum_d(b);
   if ((tid & 63) == 0) {
