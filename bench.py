@@ -79,6 +79,9 @@ def parse():
                          "tolerance line, BASELINE configs 2 and 5)")
     ap.add_argument("--conv-grouping", choices=("on", "off"), default="off",
                     help="one launch for the direct-3x3 convs of a depth level (A/B)")
+    ap.add_argument("--lazy-bn", choices=("on", "off"), default="on",
+                    help="BasicBlock bn1 normalised inside conv2's staging, never stored "
+                         "(vae2.ops.LazyBN; A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
     ap.add_argument("--full-step", action="store_true",
@@ -234,6 +237,9 @@ def main():
     if args.conv_grouping == "on":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_grouping(1)
+    if args.lazy_bn == "off":
+        from vae2 import ops as vops
+        vops.LAZY_BN = False
     if args.dtype == "bf16":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_mfma_bf16(1)

@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 8
+#define VAE2_ABI_VERSION 9
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -134,6 +134,33 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
                     const float* bias, float* y, const vae2_act* yd, int k,
                     int stride, int pad, float beta, float* stats,
                     void* stream);
+
+/* BatchNorm fused into the consumer conv (ABI 9).  A conv2d whose input is the
+ * normalised output relu?(x*scale + shift) of a training-mode BatchNorm (+ReLU) layer
+ * (BasicBlock's bn1 -> relu -> conv2, enc_hrnet.py:46-55) can read that layer's pre-BN
+ * tensor x and its save [4][C] = (mean, invstd, scale, shift) instead, so the normalised
+ * activation is never stored: _fwd_bnin / _bwd_weight_bnin are vae2_conv2d_fwd /
+ * vae2_conv2d_bwd_weight of that input (bit-identical to normalising first), legal when
+ * vae2_conv2d_bnin_ok (the LDS-tiled direct 3x3 kernels run).  Its data gradient can
+ * also produce the BatchNorm layer's backward partials [2][rows][C] (sum g, sum g*xhat
+ * with g the incoming gradient masked by the ReLU, as vae2_bn_relu_bwd_reduce writes)
+ * in the epilogue: rows = vae2_conv2d_bwd_data_bnpart_rows (0 = not available for
+ * this geometry); bn_x = the BatchNorm's pre-BN input (shape of dx).               */
+int vae2_conv2d_bnin_ok(const float* x, const vae2_act* xd, const vae2_act* yd, int k,
+                        int stride, int pad);
+int vae2_conv2d_fwd_bnin(const float* x, const vae2_act* xd, const float* bn_save, int relu,
+                         const float* wp, const float* bias, float* y, const vae2_act* yd,
+                         int k, int stride, int pad, float beta, float* stats, void* stream);
+int vae2_conv2d_bwd_weight_bnin(const float* x, const vae2_act* xd, const float* bn_save,
+                                int relu, const float* dy, const vae2_act* dyd, float* dw,
+                                float* dbias, int k, int stride, int pad, int accumulate,
+                                float* ws, int64_t ws_size, void* stream);
+int64_t vae2_conv2d_bwd_data_bnpart_rows(const float* dy, const vae2_act* dyd,
+                                         const vae2_act* dxd, int k, int stride, int pad);
+int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const float* wp,
+                                float* dx, const vae2_act* dxd, int k, int stride, int pad,
+                                const float* bn_x, const vae2_act* bn_xd, const float* bn_save,
+                                int relu, float* partials, void* stream);
 
 /* Name of the kernel instantiation a vae2_conv2d_fwd launch with this geometry
  * uses (e.g. "igemm_kernel<4, 4, true, 0>"), for matching timings with rocprof. */

@@ -73,6 +73,7 @@ DIRECT_SHAPES = [
     (2, 5, 7, 3, 5, False),       # image smaller than one tile, TM = 2
     (1, 8, 32, 154, 144, False),  # 5 slabs (39 quads), N split over 3 blocks
     (2, 6, 33, 256, 18, True),    # 8 slabs, 2 column tiles of which one has 1 column
+    (2, 16, 32, 72, 72, False),   # weight gradient: 2 co slabs of 32 MFMA + 4 VALU rows
     # 1x1 (the direct weight-gradient kernel's KS = 1 form; data paths: gather kernel)
     (2, 8, 40, 270, 270, True, 1),
     (1, 4, 64, 64, 256, False, 1),

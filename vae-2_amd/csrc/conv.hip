@@ -402,6 +402,19 @@ struct DConv {
   int y_ps;
   float beta;
   float* stats;  // [2][gridDim.x][n] or null
+  // Forward (FLIP = false): the input is the pre-BN output of a BatchNorm(+ReLU) layer
+  // whose normalised activation is never stored: staging applies relu?(a*scale + shift)
+  // (isave = that layer's (mean, invstd, scale, shift) [4][a_c]) to in-image pixels, the
+  // zero halo stays zero.
+  const float* isave;
+  int irelu;
+  // Data gradient (FLIP = true): this output is the gradient of such a layer's (never
+  // stored) output; the epilogue writes that layer's BatchNorm backward partials (sum g,
+  // sum g*xhat; g = the gradient masked by its ReLU) into stats instead of (sum, sum^2).
+  // bx = the layer's pre-BN tensor (same pixels and channels as y), bsave its [4][n].
+  const float* bx;
+  int bx_ps, brelu;
+  const float* bsave;
 };
 
 constexpr int kDcBW = 32;     // tile columns
@@ -520,9 +533,20 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const int sq = threadIdx.x % qs, pb = threadIdx.x / qs, pstride = 256 / qs;
     const int c = (q0 + sq) * 4;
     const bool cpad = c + 4 > p.a_c;
+    // input BatchNorm (FLIP = false only): this thread's channel quad's scale / shift
+    f4 isc, ish;
+    if (!FLIP && p.isave) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ch = c + k < p.a_c ? c + k : p.a_c - 1;
+        isc[k] = p.isave[2 * p.a_c + ch];
+        ish[k] = p.isave[3 * p.a_c + ch];
+      }
+    }
     if (pb < pstride) {
       for (int pix0 = pb; pix0 < LH * LW; pix0 += SB * pstride) {
         f4 v[SB];
+        bool okv[SB];
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
           const int pix = pix0 + u * pstride;
@@ -530,6 +554,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
           const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
           const bool ok = pix < LH * LW && (unsigned)ih < (unsigned)p.img_h &&
                           (unsigned)iw < (unsigned)p.img_w;
+          okv[u] = ok;
           if (VAE2_ABLATE & 1) v[u] = f4{(float)pix, (float)ih, (float)iw, (float)c};
           else
           v[u] = load4(arsrc, ok ? (uint32_t)(((img_base + ih) * p.img_w + iw) * p.a_ps + c) * 4u
@@ -539,6 +564,13 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         for (int u = 0; u < SB; ++u) {
           const int pix = pix0 + u * pstride;
           if (pix >= LH * LW) break;
+          if (!FLIP && p.isave && okv[u]) {  // = bn_apply_body's arithmetic
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float t = __builtin_fmaf(v[u][k], isc[k], ish[k]);
+              v[u][k] = (p.irelu && t < 0.f) ? 0.f : t;
+            }
+          }
           if (cpad) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -616,8 +648,19 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
 
   // ---- epilogue (bias, beta*y, BN partial statistics) ----
   float csum[TN], csq[TN];
+  // producer BatchNorm backward partials (FLIP with bx): per-column mean, invstd, scale,
+  // shift of that layer (= bn_bwd_reduce_body's arithmetic, element by element)
+  const bool bnp = FLIP && p.bx != nullptr;
+  float bmn[TN], bis[TN], bsc[TN], bsh[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f; csq[j] = 0.f;
+    if (bnp) {
+      const int n = n0 + j * 16 + r < p.n ? n0 + j * 16 + r : p.n - 1;
+      bmn[j] = p.bsave[n]; bis[j] = p.bsave[p.n + n];
+      bsc[j] = p.bsave[2 * p.n + n]; bsh[j] = p.bsave[3 * p.n + n];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int oh = oh0 + wave * (TM / 2) + (i >> 1);
@@ -625,7 +668,9 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     for (int e = 0; e < 4; ++e) {
       const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
       if (oh >= p.img_h || ow >= p.img_w) continue;
-      float* yrow = p.y + (int64_t)((img_base + oh) * p.img_w + ow) * p.y_ps;
+      const int64_t pix = (int64_t)(img_base + oh) * p.img_w + ow;
+      float* yrow = p.y + pix * p.y_ps;
+      const float* xrow = bnp ? p.bx + pix * p.bx_ps : nullptr;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + j * 16 + r;
@@ -634,8 +679,15 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         if (p.bias) v += p.bias[n];
         if (p.beta != 0.f) v += p.beta * yrow[n];
         if (!(VAE2_ABLATE & 2) || v == 1234.5f) yrow[n] = v;
-        csum[j] += v;
-        csq[j] += v * v;
+        if (bnp) {
+          const float xv = xrow[n];
+          const float gv = (p.brelu && !(__builtin_fmaf(xv, bsc[j], bsh[j]) > 0.f)) ? 0.f : v;
+          csum[j] += gv;
+          csq[j] += gv * (xv - bmn[j]) * bis[j];
+        } else {
+          csum[j] += v;
+          csq[j] += v * v;
+        }
       }
     }
   }
@@ -645,15 +697,25 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const int oh = oh0 + rtrow, ow = ow0 + rtcol;
     const bool in = oh < p.img_h && ow < p.img_w;
     const int nb = n0 + BN + rh * NRL;
-    float* yrow = p.y + (int64_t)((img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0)) * p.y_ps + nb;
+    const int64_t pix = (int64_t)(img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0);
+    float* yrow = p.y + pix * p.y_ps + nb;
 #pragma unroll
     for (int j = 0; j < NRL; ++j) {
       float v = racc[j];
       if (p.bias) v += p.bias[nb + j];
       if (p.beta != 0.f && in) v += p.beta * yrow[j];
       if (in && (!(VAE2_ABLATE & 2) || v == 1234.5f)) yrow[j] = v;
-      rsum[j] = in ? v : 0.f;
-      rsq[j] = in ? v * v : 0.f;
+      if (bnp) {
+        const int n = nb + j;
+        const float xv = in ? p.bx[pix * p.bx_ps + n] : 0.f;
+        const float gv = (p.brelu && !(__builtin_fmaf(xv, p.bsave[2 * p.n + n],
+                                                      p.bsave[3 * p.n + n]) > 0.f)) ? 0.f : v;
+        rsum[j] = in ? gv : 0.f;
+        rsq[j] = in ? gv * (xv - p.bsave[n]) * p.bsave[p.n + n] : 0.f;
+      } else {
+        rsum[j] = in ? v : 0.f;
+        rsq[j] = in ? v * v : 0.f;
+      }
     }
   }
   if (p.stats) {
@@ -1055,21 +1117,36 @@ struct WGrad3 {
   int csw, n_ci_slabs;  // channels per ci slab (multiple of 4), slabs
   uint32_t x_bytes, dy_bytes;
   float* part;  // [splits][cout][9*cin4]
+  // x is the pre-BN output of a BatchNorm(+ReLU) layer whose normalised activation is
+  // never stored (DConv::isave): staging applies relu?(x*scale + shift) to in-image pixels
+  const float* isave;
+  int irelu;
 };
 
-template <int TM, int TN, int BH, bool PF, int KS, bool BF = false>
+// NR > 0 (fp32 operands, one co slab): cout = 16*TM + NR (the 18 / 36-channel layers)
+// -- the last NR output channels are computed on the VALU beside the MFMAs instead of in a
+// further 16-row MFMA tile that would be mostly padding: every lane already holds the X
+// fragment of its column for 4 pixels (the MFMA B operand), so it adds those pixels'
+// dY[co][px] * X products for each remainder co (dY rows staged with the others) and
+// the 4 lane groups' sums are combined at the end.  The MFMA work of an 18-channel
+// layer halves (32 -> 16 rows), of a 36-channel one drops by 1/3.  With several co slabs
+// (72 = 2 x (32 + 4)) each slab is 16*TM + NR channels wide.
+template <int TM, int TN, int BH, bool PF, int KS, bool BF = false, int NR = 0>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   constexpr int HALO = KS / 2, TAPS = KS * KS;
   constexpr int LH = BH + KS - 1, LW = 32 + KS - 1, NPX = BH * 32, LPX = LH * LW;
   constexpr int QMAX = KS == 1 ? 16 : 9;  // channel quads per slab
   constexpr int DYS = NPX + 4;  // dY^T row stride (floats)
+  constexpr int NRQ = (NR + 3) / 4;        // remainder co quads staged
+  constexpr int NQ = 4 * TM + NRQ;         // dY co quads staged per tile
+  static_assert(NR == 0 || (!BF && NR <= 4), "remainder shape");
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* dyt = sm;                  // [16*TM][DYS]
-  float* xt = sm + 16 * TM * DYS;   // [csw + 1][LPX], row csw = zeros
+  float* dyt = sm;                  // [16*TM + 4*NRQ][DYS]
+  float* xt = sm + NQ * 4 * DYS;    // [csw + 1][LPX], row csw = zeros
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int cis = blockIdx.y % p.n_ci_slabs, cos = blockIdx.y / p.n_ci_slabs;
-  const int co0 = cos * 16 * TM, c0 = cis * p.csw;
+  const int co0 = cos * (16 * TM + NR), c0 = cis * p.csw;
   const int csw_real = p.cin4 - c0 < p.csw ? p.cin4 - c0 : p.csw;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
@@ -1084,21 +1161,43 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     bbase[j] = ok ? cl * LPX + (t / KS) * LW + (t % KS) : p.csw * LPX;
   }
   for (int i = threadIdx.x; i < LPX; i += 256) xt[p.csw * LPX + i] = 0.f;
+  // input BatchNorm: the slab's scale / shift (read after the tile loop's first barrier)
+  __shared__ float ibn[2][QMAX * 4];
+  if (p.isave && threadIdx.x < QMAX * 4) {
+    const int ch = c0 + (int)threadIdx.x < p.cin ? c0 + (int)threadIdx.x : p.cin - 1;
+    ibn[0][threadIdx.x] = p.isave[2 * p.cin + ch];
+    ibn[1][threadIdx.x] = p.isave[3 * p.cin + ch];
+  }
+  auto ibn_apply = [&](f4& v, int q) {  // = bn_apply_body's arithmetic
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = __builtin_fmaf(v[k], ibn[0][4 * q + k], ibn[1][4 * q + k]);
+      v[k] = (p.irelu && t < 0.f) ? 0.f : t;
+    }
+  };
 
   f4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float racc[TN][NR > 0 ? NR : 1];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < NR; ++q) racc[j][q] = 0.f;
 
   const int per_img = p.tiles_h * p.tiles_w;
   const int tb = blockIdx.x * p.tiles_per_split;
   const int te = tb + p.tiles_per_split < p.ntiles ? tb + p.tiles_per_split : p.ntiles;
   // Register prefetch: tile t+1's global loads are in flight while tile t computes.
-  constexpr int NI = NPX * 4 * TM / 256;     // dY items per thread
+  constexpr int NDY = NPX * NQ;                 // dY items (f4 = 4 co of one pixel)
+  constexpr int NI = (NDY + 255) / 256;         // dY items per thread
   constexpr int NX = (LPX * QMAX + 255) / 256;  // X items per thread
   const int xtotal = LPX * (csw_real >> 2);
   f4 pdy[NI], pxx[NX];
+  static_assert(NX <= 32, "x item mask");
+  uint32_t xok = 0;  // in-image x items of the prefetched tile (input BatchNorm)
   auto fetch = [&](int tile) {
     const int img = tile / per_img;
     const int trem = tile - img * per_img;
@@ -1111,7 +1210,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
       const int q = i / NPX, px = i - q * NPX;
       const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
       const int co = co0 + 4 * q;
-      const bool ok = oh < p.h && ow < p.w && co < p.cout;
+      const bool ok = i < NDY && oh < p.h && ow < p.w && co < p.cout;
       pdy[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co) * 4u : kOOB);
     }
 #pragma unroll
@@ -1123,12 +1222,14 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
       const int c = c0 + 4 * q;
       const bool ok = i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
       pxx[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c) * 4u : kOOB);
+      xok = u == 0 ? (uint32_t)ok : (xok | ((uint32_t)ok << u));
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = threadIdx.x + u * 256;
+      if (NDY % 256 != 0 && i >= NDY) break;
       const int q = i / NPX, px = i - q * NPX;
       const int co = co0 + 4 * q;
 #pragma unroll
@@ -1140,6 +1241,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
       if (i < xtotal) {
         const int q = i / LPX, hp = i - q * LPX;
         const int c = c0 + 4 * q;
+        if (p.isave && ((xok >> u) & 1u)) ibn_apply(pxx[u], q);
 #pragma unroll
         for (int k = 0; k < 4; ++k) xt[(4 * q + k) * LPX + hp] = c + k < p.cin ? pxx[u][k] : 0.f;
       }
@@ -1164,12 +1266,13 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
           const int q = i / NPX, px = i - q * NPX;
           const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
           const int co = co0 + 4 * q;
-          const bool ok = oh < p.h && ow < p.w && co < p.cout;
+          const bool ok = i < NDY && oh < p.h && ow < p.w && co < p.cout;
           v[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co) * 4u : kOOB);
         }
 #pragma unroll
         for (int u = 0; u < NI; ++u) {
           const int i = threadIdx.x + u * 256;
+          if (NDY % 256 != 0 && i >= NDY) break;
           const int q = i / NPX, px = i - q * NPX;
           const int co = co0 + 4 * q;
 #pragma unroll
@@ -1179,6 +1282,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
       }
       for (int i0 = threadIdx.x; i0 < xtotal; i0 += 4 * 256) {
         f4 v[4];
+        bool okv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = i0 + u * 256;
@@ -1188,6 +1292,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
           const int c = c0 + 4 * q;
           const bool ok =
               i < xtotal && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w;
+          okv[u] = ok;
           v[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c) * 4u : kOOB);
         }
 #pragma unroll
@@ -1196,6 +1301,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
           if (i >= xtotal) break;
           const int q = i / LPX, hp = i - q * LPX;
           const int c = c0 + 4 * q;
+          if (p.isave && okv[u]) ibn_apply(v[u], q);
 #pragma unroll
           for (int k = 0; k < 4; ++k) xt[(4 * q + k) * LPX + hp] = c + k < p.cin ? v[u][k] : 0.f;
         }
@@ -1228,6 +1334,20 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+        if constexpr (NR > 0) {  // this lane's 4 pixels x its columns, remainder rows
+          const int px0 = ch * 16 + 4 * g;
+#pragma unroll
+          for (int q = 0; q < NR; ++q) {
+            const f4 d = *reinterpret_cast<const f4*>(&dyt[(16 * TM + q) * DYS + px0]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              racc[j][q] = __builtin_fmaf(d[0], fb[j][0], racc[j][q]);
+              racc[j][q] = __builtin_fmaf(d[1], fb[j][1], racc[j][q]);
+              racc[j][q] = __builtin_fmaf(d[2], fb[j][2], racc[j][q]);
+              racc[j][q] = __builtin_fmaf(d[3], fb[j][3], racc[j][q]);
+            }
+          }
+        }
       }
     } else {  // bf16 operands: one 16x16x32 MFMA per pair of 16-pixel chunks
 #pragma unroll 2
@@ -1261,6 +1381,22 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
         const int co = co0 + i * 16 + g * 4 + e;
         if (co < p.cout) out[(int64_t)co * ncol4 + col] = acc[i][j][e];
       }
+  }
+  if constexpr (NR > 0) {  // the 4 lane groups' pixel sums (fixed order), rows 16*TM + q
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = (wave * TN + j) * 16 + r;
+      const int t = n / p.csw;
+      const int cl = n - t * p.csw;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        float v = racc[j][q];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (g == 0 && t < TAPS && cl < csw_real)
+          out[(int64_t)(co0 + 16 * TM + q) * ncol4 + t * p.cin4 + c0 + cl] = v;
+      }
+    }
   }
 }
 
@@ -1502,9 +1638,20 @@ static bool dconv_use(const vae2_act* ad, const vae2_act* yd, int k, int stride,
   return ad->w >= 16 && ad->n * d.tiles_h * d.tiles_w * d.nblk >= 256;
 }
 
+// BatchNorm fused at a direct-3x3 conv's input (DConv::isave / irelu) or, for its data
+// gradient, that BatchNorm's backward partials in the epilogue (DConv::bx ...).
+struct BnSide {
+  const float* isave = nullptr;
+  int irelu = 0;
+  const float* bx = nullptr;
+  int bx_ps = 0, brelu = 0;
+  const float* bsave = nullptr;
+};
+
 int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta,
-                 float* stats, bool flip, hipStream_t s, const char* fn);
+                 float* stats, bool flip, hipStream_t s, const char* fn,
+                 const BnSide& bn = BnSide{});
 
 #if VAE2_PART(2)
 template <int TM, bool FLIP>
@@ -1564,7 +1711,7 @@ static void dconv_group_launch_tn(const DConvGroup& g, int tn, dim3 grid, size_t
 
 int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta,
-                 float* stats, bool flip, hipStream_t s, const char* fn) {
+                 float* stats, bool flip, hipStream_t s, const char* fn, const BnSide& bn) {
   DTile d = pick_dtile(ad, yd);
   DConv p{};
   p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
@@ -1573,6 +1720,8 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.w = wp; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
   p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
   p.stats = stats;
+  p.isave = bn.isave; p.irelu = bn.irelu;
+  p.bx = bn.bx; p.bx_ps = bn.bx_ps; p.brelu = bn.brelu; p.bsave = bn.bsave;
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
   const size_t shm = dconv_shm(d);
   if (d.tm == 4) {
@@ -1596,6 +1745,7 @@ static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
 struct W3Tile {
   int ks, tm, tn, bh, csw, n_ci_slabs, n_co_slabs, tiles_h, tiles_w, ntiles, tps, splits;
   bool pf;
+  int nr = 0;  // output channels on the VALU beside the MFMA rows (wgrad3_kernel NR)
 };
 
 static bool wgrad3_shape_ok(const vae2_act* xd, const vae2_act* dyd, int k, int stride, int pad) {
@@ -1618,6 +1768,13 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
   const int mt = (int)((dyd->c + 15) / 16);
   t.n_co_slabs = (mt + 3) / 4;
   t.tm = (mt + t.n_co_slabs - 1) / t.n_co_slabs;
+  // 18 / 36 / 72 output channels: co slabs of 16 + 2, 32 + 4, 2 x (32 + 4): MFMA rows
+  // plus VALU rows (fp32 operands)
+  if (k == 3 && g_dconv_nr && !g_bf16 && (dyd->c == 18 || dyd->c == 36 || dyd->c == 72)) {
+    t.tm = dyd->c == 18 ? 1 : 2;
+    t.nr = dyd->c == 18 ? 2 : 4;
+    t.n_co_slabs = (int)(dyd->c / (16 * t.tm + t.nr));
+  }
   t.bh = (t.tm <= 2 && t.csw <= 24 && k == 3) ? 8 : 4;
   t.tiles_h = (int)ceil_div(dyd->h, t.bh);
   t.tiles_w = (int)ceil_div(dyd->w, 32);
@@ -1647,13 +1804,26 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
 
 static size_t wgrad3_lds(const W3Tile& t) {
   const int npx = t.bh * 32, lpx = (t.bh + t.ks - 1) * (32 + t.ks - 1);
-  return ((size_t)16 * t.tm * (npx + 4) + (size_t)(t.csw + 1) * lpx) * sizeof(float);
+  const int rows = 16 * t.tm + 4 * ((t.nr + 3) / 4);
+  return ((size_t)rows * (npx + 4) + (size_t)(t.csw + 1) * lpx) * sizeof(float);
 }
 
 #if VAE2_PART(3)
 template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
-                             hipStream_t s) {
+                             hipStream_t s, int nr = 0) {
+  if constexpr (TM == 1 || TM == 2) {
+    if (nr) {  // (TM, NR) = (1, 2) or (2, 4): pick_w3tile, fp32 operands
+      constexpr int R = TM == 1 ? 2 : 4;
+      switch (tn) {
+#define CASE(T) \
+  case T: VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, false, R>), grid, dim3(256), shm, s, p); break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
+#undef CASE
+      }
+      return;
+    }
+  }
   if (ks == 1) {  // 1x1: at most 64 channels = 4 column tiles per slab, one per wave
     if (g_bf16) VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1, true>), grid, dim3(256), shm, s, p);
     else VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
@@ -1674,8 +1844,8 @@ template <int BH, bool PF>
 static void wgrad3_launch_tm(const WGrad3& p, const W3Tile& t, dim3 grid, size_t shm,
                              hipStream_t s) {
   switch (t.tm) {
-    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
-    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
+    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr); break;
+    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr); break;
     case 3: wgrad3_launch_tn<3, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
     default: wgrad3_launch_tn<4, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
   }
@@ -1848,6 +2018,56 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
   p.beta = beta;
   p.stats = stats;
   return launch_igemm(p, 0, as_stream(stream), fn);
+}
+
+int vae2_conv2d_bnin_ok(const float* x, const vae2_act* xd, const vae2_act* yd, int k,
+                        int stride, int pad) {
+  if (!x || !conv_shapes_ok(xd, yd, k, stride, pad) || !fits32(xd) || !fits32(yd)) return 0;
+  return dconv_use(xd, yd, k, stride, pad, x) && g_conv_algo != 1 &&
+         wgrad3_shape_ok(xd, yd, k, stride, pad) && vec_ok(x, (int)xd->ps);
+}
+
+int vae2_conv2d_fwd_bnin(const float* x, const vae2_act* xd, const float* bn_save, int relu,
+                         const float* wp, const float* bias, float* y, const vae2_act* yd,
+                         int k, int stride, int pad, float beta, float* stats, void* stream) {
+  const char* fn = "vae2_conv2d_fwd_bnin";
+  VAE2_REQUIRE(x && wp && y && bn_save, fn, "null pointer");
+  VAE2_REQUIRE(conv_shapes_ok(xd, yd, k, stride, pad), fn, "inconsistent conv shapes");
+  VAE2_REQUIRE(vae2_conv2d_bnin_ok(x, xd, yd, k, stride, pad), fn,
+               "input BatchNorm needs the direct 3x3 kernels (vae2_conv2d_bnin_ok)");
+  BnSide bn;
+  bn.isave = bn_save;
+  bn.irelu = relu ? 1 : 0;
+  return launch_dconv(x, xd, wp, (uint32_t)(vae2_conv2d_packed_size(yd->c, xd->c, k, 0) * 4),
+                      bias, y, yd, beta, stats, false, as_stream(stream), fn, bn);
+}
+
+int64_t vae2_conv2d_bwd_data_bnpart_rows(const float* dy, const vae2_act* dyd,
+                                         const vae2_act* dxd, int k, int stride, int pad) {
+  if (!dy || !conv_shapes_ok(dxd, dyd, k, stride, pad) || !fits32(dxd) || !fits32(dyd))
+    return 0;
+  return dconv_use(dyd, dxd, k, stride, pad, dy) ? dconv_rows(dyd, dxd) : 0;
+}
+
+int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const float* wp,
+                                float* dx, const vae2_act* dxd, int k, int stride, int pad,
+                                const float* bn_x, const vae2_act* bn_xd, const float* bn_save,
+                                int relu, float* partials, void* stream) {
+  const char* fn = "vae2_conv2d_bwd_data_bnpart";
+  VAE2_REQUIRE(dy && wp && dx && bn_x && bn_xd && bn_save && partials, fn, "null pointer");
+  VAE2_REQUIRE(conv_shapes_ok(dxd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
+  VAE2_REQUIRE(bn_xd->n == dxd->n && bn_xd->h == dxd->h && bn_xd->w == dxd->w &&
+               bn_xd->c == dxd->c && bn_xd->ps >= bn_xd->c && fits32(bn_xd), fn,
+               "BatchNorm input shape must match dx");
+  VAE2_REQUIRE(vae2_conv2d_bwd_data_bnpart_rows(dy, dyd, dxd, k, stride, pad) > 0, fn,
+               "BatchNorm partials need the direct 3x3 kernel (vae2_conv2d_bwd_data_bnpart_rows)");
+  BnSide bn;
+  bn.bx = bn_x;
+  bn.bx_ps = (int)bn_xd->ps;
+  bn.bsave = bn_save;
+  bn.brelu = relu ? 1 : 0;
+  return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
+                      nullptr, dx, dxd, 0.f, partials, true, as_stream(stream), fn, bn);
 }
 
 int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
@@ -2031,11 +2251,11 @@ int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, 
   return part + bias_part + 4;
 }
 
-int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* dy,
-                              const vae2_act* dyd, float* dw, int64_t dw_ld, float* dbias,
-                              int k, int stride, int pad, int accumulate, float* ws,
-                              int64_t ws_size, void* stream) {
-  const char* fn = "vae2_conv2d_bwd_weight";
+static int bwd_weight_impl(const float* x, const vae2_act* xd, const float* dy,
+                           const vae2_act* dyd, float* dw, int64_t dw_ld, float* dbias,
+                           int k, int stride, int pad, int accumulate, float* ws,
+                           int64_t ws_size, void* stream, const float* isave, int irelu,
+                           const char* fn) {
   VAE2_REQUIRE(xd && dw_ld >= xd->c * k * k, fn, "bad dW row stride");
   VAE2_REQUIRE(x && dy && dw && ws, fn, "null pointer");
   VAE2_REQUIRE(conv_shapes_ok(xd, dyd, k, stride, pad), fn, "inconsistent conv shapes");
@@ -2045,8 +2265,11 @@ int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* d
   const int cin4 = round_up((int)xd->c, 4);
   const int ncol4 = k * k * cin4;
   int splits = 0;
-  if (g_conv_algo != 1 && wgrad3_shape_ok(xd, dyd, k, stride, pad) && vec_ok(x, (int)xd->ps) &&
-      vec_ok(dy, (int)dyd->ps)) {
+  const bool direct = g_conv_algo != 1 && wgrad3_shape_ok(xd, dyd, k, stride, pad) &&
+                      vec_ok(x, (int)xd->ps) && vec_ok(dy, (int)dyd->ps);
+  VAE2_REQUIRE(direct || !isave, fn,
+               "input BatchNorm needs the direct 3x3 weight-gradient kernel (vae2_conv2d_bnin_ok)");
+  if (direct) {
     W3Tile t3 = pick_w3tile(xd, dyd, k);
     WGrad3 q{};
     q.x = x; q.x_ps = (int)xd->ps; q.cin = (int)xd->c; q.cin4 = cin4;
@@ -2057,6 +2280,8 @@ int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* d
     q.csw = t3.csw; q.n_ci_slabs = t3.n_ci_slabs;
     q.x_bytes = act_bytes(xd); q.dy_bytes = act_bytes(dyd);
     q.part = ws;
+    q.isave = isave;
+    q.irelu = irelu ? 1 : 0;
     dim3 grid((unsigned)t3.splits, (unsigned)(t3.n_ci_slabs * t3.n_co_slabs));
     const size_t shm = wgrad3_lds(t3);
     if (t3.bh == 8) wgrad3_launch<8>(q, t3, grid, shm, s);
@@ -2119,6 +2344,24 @@ reduce:
     if (rc) return rc;
   }
   return 0;
+}
+
+int vae2_conv2d_bwd_weight_ld(const float* x, const vae2_act* xd, const float* dy,
+                              const vae2_act* dyd, float* dw, int64_t dw_ld, float* dbias,
+                              int k, int stride, int pad, int accumulate, float* ws,
+                              int64_t ws_size, void* stream) {
+  return bwd_weight_impl(x, xd, dy, dyd, dw, dw_ld, dbias, k, stride, pad, accumulate, ws,
+                         ws_size, stream, nullptr, 0, "vae2_conv2d_bwd_weight");
+}
+
+int vae2_conv2d_bwd_weight_bnin(const float* x, const vae2_act* xd, const float* bn_save,
+                                int relu, const float* dy, const vae2_act* dyd, float* dw,
+                                float* dbias, int k, int stride, int pad, int accumulate,
+                                float* ws, int64_t ws_size, void* stream) {
+  const char* fn = "vae2_conv2d_bwd_weight_bnin";
+  if (!xd || !bn_save) return fail(fn, "null pointer");
+  return bwd_weight_impl(x, xd, dy, dyd, dw, xd->c * k * k, dbias, k, stride, pad, accumulate,
+                         ws, ws_size, stream, bn_save, relu, fn);
 }
 
 int vae2_conv2d_bwd_weight(const float* x, const vae2_act* xd, const float* dy,

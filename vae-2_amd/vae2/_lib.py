@@ -65,6 +65,14 @@ _SIGS = {
                                             c_i64]),
     "vae2_conv2d_bwd_data": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                      c_f32, c_vp]),
+    "vae2_conv2d_bnin_ok": (c_int, [c_vp, P_ACT, P_ACT, c_int, c_int, c_int]),
+    "vae2_conv2d_fwd_bnin": (c_int, [c_vp, P_ACT, c_vp, c_int, c_vp, c_vp, c_vp, P_ACT, c_int,
+                                     c_int, c_int, c_f32, c_vp, c_vp]),
+    "vae2_conv2d_bwd_weight_bnin": (c_int, [c_vp, P_ACT, c_vp, c_int, c_vp, P_ACT, c_vp, c_vp,
+                                            c_int, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
+    "vae2_conv2d_bwd_data_bnpart_rows": (c_i64, [c_vp, P_ACT, P_ACT, c_int, c_int, c_int]),
+    "vae2_conv2d_bwd_data_bnpart": (c_int, [c_vp, P_ACT, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
+                                            c_vp, P_ACT, c_vp, c_int, c_vp, c_vp]),
     "vae2_conv2d_bwd_weight_ws_size": (c_i64, [P_ACT, P_ACT, c_int]),
     "vae2_conv2d_bwd_weight": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, c_vp, c_int, c_int,
                                        c_int, c_int, c_vp, c_i64, c_vp]),
@@ -159,7 +167,7 @@ _SIGS = {
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _lib = None
 
 

@@ -118,10 +118,16 @@ def run_blocks_lockstep(blocks, xs):
     if not all(isinstance(b, BasicBlock) and b.downsample is None for b in blocks):
         return [b.run(x) for b, x in zip(blocks, xs)]
     links = [ops.GradLink(2) for _ in blocks]  # x feeds conv1 and the shortcut
+    # bn1's normalised output feeds only conv2: conv2 normalises it while staging its input
+    # (ops.LazyBN) where the direct 3x3 kernels run, so it is never stored
+    res_ok = all(ops._bn_quad_ok(x) for x in xs)
+    lazy = [ops.LazyBN() if res_ok and ops.lazy_bn_ok(tuple(x.shape[:3]) + (b.conv1.out_channels,),
+                                                      b.conv2) else None
+            for b, x in zip(blocks, xs)]
     outs = ops.conv_bn_multi(xs, [b.conv1 for b in blocks], [b.bn1 for b in blocks], True,
-                             x_links=links)
+                             x_links=links, bn_outs=lazy)
     return ops.conv_bn_multi(outs, [b.conv2 for b in blocks], [b.bn2 for b in blocks], True,
-                             residuals=xs, res_links=links)
+                             residuals=xs, res_links=links, bn_ins=lazy)
 
 
 def _shortcut(cin, cout, stride):

@@ -135,12 +135,48 @@ class GradLink:
         return buf
 
 
+# ------------------------------------------------- BN fused into the consumer ----
+class LazyBN:
+    """A training-mode BatchNorm(+ReLU) layer whose normalised output z is never stored
+    (BasicBlock's bn1 -> relu -> conv2, enc_hrnet.py:46-55): its _ConvBNMulti level
+    returns the pre-BN conv output r in z's place, the consumer conv normalises r while
+    staging its input (vae2_conv2d_fwd_bnin; the weight gradient likewise,
+    vae2_conv2d_bwd_weight_bnin), and the consumer's data gradient -- the gradient of z
+    -- writes this layer's backward partials in its epilogue
+    (vae2_conv2d_bwd_data_bnpart), so neither the forward apply pass nor the backward
+    reduce pass runs for it.  `save` = the layer's (mean, invstd, scale, shift)."""
+
+    __slots__ = ("save", "relu", "part", "rows")
+
+    def __init__(self):
+        self.save, self.relu, self.part, self.rows = None, False, None, 0
+
+
+LAZY_BN = True  # False: every BatchNorm output is stored (A/B and parity tests)
+
+
+def lazy_bn_ok(shape, conv):
+    """Can `conv` (3x3 stride 1) consume a LazyBN output of NHWC `shape` (N,H,W,C)?
+    (the direct 3x3 forward and weight-gradient kernels must run for it)"""
+    if not LAZY_BN or not torch.cuda.is_available():
+        return False
+    n, h, w, c = shape
+    k, st, pad = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+    if conv.in_channels != c:
+        return False
+    oh, ow = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+    xa = Act(n, h, w, c, (c + 3) // 4 * 4)  # a new_act's layout (16-byte aligned pixels)
+    ya = Act(n, oh, ow, conv.out_channels, (conv.out_channels + 3) // 4 * 4)
+    return bool(_lib.load().vae2_conv2d_bnin_ok(ctypes.c_void_p(256), ctypes.byref(xa),
+                                                ctypes.byref(ya), k, st, pad))
+
+
 # --------------------------------------------------------------- conv + BN ----
 class ConvSpec:
     """Static description of a conv(+BN) call: geometry and module handles."""
 
     __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training", "x_link",
-                 "res_link")
+                 "res_link", "bn_in", "bn_out")
 
     def __init__(self, conv, bn=None, relu=False):
         kh, kw = conv.kernel_size
@@ -152,6 +188,7 @@ class ConvSpec:
         self.relu = relu
         self.bn = bn
         self.x_link = self.res_link = None
+        self.bn_in = self.bn_out = None  # LazyBN: BatchNorm fused into the consumer conv
         if bn is not None:
             if bn.momentum is None:
                 raise ValueError("cumulative-average BatchNorm (momentum=None) is not supported")
@@ -341,7 +378,8 @@ def _merge(notes):
 
 
 def _conv_fwd_queued(group, x, weight, bias, spec, stats):
-    """_conv_fwd, queued on a ConvGroup."""
+    """_conv_fwd, queued on a ConvGroup (a LazyBN input: launched at once, normalised
+    while staged)."""
     xp, xa = act_of(x)
     n, h, w, _ = x.shape
     oh, ow = spec.out_hw(h, w)
@@ -350,6 +388,12 @@ def _conv_fwd_queued(group, x, weight, bias, spec, stats):
     yp, ya = act_of(y)
     if prof.active():
         _conv_work("fwd", xa, (n, oh, ow, cout), spec.k, spec.stride)
+    lz = spec.bn_in
+    if lz is not None:
+        call("vae2_conv2d_fwd_bnin", xp, ctypes.byref(xa), ptr(lz.save), int(lz.relu),
+             ptr(packed_weight(weight, 0)), ptr(bias), yp, ctypes.byref(ya), spec.k,
+             spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
+        return y
     group.add(0, xp, xa, packed_weight(weight, 0), bias, yp, ya, spec, 0.0, stats)
     return y
 
@@ -422,8 +466,14 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         ws = _empty((max(size, 1),), x)
         if prof.active():
             _conv_work("wgrad", xa, tuple(dy.shape), spec.k, spec.stride)
-        call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya), ptr(wsink),
-             ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
+        lz = spec.bn_in
+        if lz is not None:
+            call("vae2_conv2d_bwd_weight_bnin", xp, ctypes.byref(xa), ptr(lz.save),
+                 int(lz.relu), dyp, ctypes.byref(dya), ptr(wsink), ptr(bsink), spec.k,
+                 spec.stride, spec.pad, 1, ptr(ws), size, s)
+        else:
+            call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya),
+                 ptr(wsink), ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
         if _WGRAD_BATCH[0]:
             # the deferred reduction writes wsink at the flush: a temporary dW target
             # must outlive it like the workspace
@@ -444,7 +494,18 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         wp = packed_weight(weight, 1)
         if prof.active():
             _conv_work("dgrad", xa, tuple(dy.shape), spec.k, spec.stride)
-        if group is not None:
+        lz = spec.bn_in
+        rows = 0
+        if lz is not None and beta == 0.0:
+            rows = _lib.load().vae2_conv2d_bwd_data_bnpart_rows(
+                dyp, ctypes.byref(dya), ctypes.byref(dxa), spec.k, spec.stride, spec.pad)
+        if rows > 0:  # + the LazyBN layer's backward partials (its reduce pass skipped)
+            part = _empty((2 * rows * xa.c,), x)
+            call("vae2_conv2d_bwd_data_bnpart", dyp, ctypes.byref(dya), ptr(wp), dxp,
+                 ctypes.byref(dxa), spec.k, spec.stride, spec.pad, xp, ctypes.byref(xa),
+                 ptr(lz.save), int(lz.relu), ptr(part), s)
+            lz.part, lz.rows = part, rows
+        elif group is not None:
             group.add(1, dyp, dya, wp, None, dxp, dxa, spec, beta)
         else:
             call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ptr(wp), dxp,
@@ -664,18 +725,23 @@ class _ConvBNMulti(torch.autograd.Function):
             from . import dist as vdist
             vdist.all_reduce_(buf, group=group)
             call("vae2_bn_multi_finalize", n, arr, s)
-        ys = []
-        lay = (_lib.BnLayer * n)()
+        ys, lay = [], []
         for i, (r, save, spec) in enumerate(zip(rs, saves, specs)):
+            lz = spec.bn_out
+            if lz is not None:  # normalised by the consumer conv: r stands in for y
+                lz.save, lz.relu, lz.part, lz.rows = save, spec.relu, None, 0
+                ys.append(r)
+                continue
             y = new_act(tuple(r.shape), r)
             ys.append(y)
             res = L[i][5]
-            lay[i] = _bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
-                               spec.relu)
-        if prof.active():
-            prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None else 2)
-                             for i, r in enumerate(rs)))
-        call("vae2_bn_multi_apply", n, lay, s)
+            lay.append(_bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
+                                 spec.relu))
+        if lay:
+            if prof.active():
+                prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None else 2)
+                                 for i, r in enumerate(rs) if specs[i].bn_out is None))
+            call("vae2_bn_multi_apply", len(lay), (_lib.BnLayer * len(lay))(*lay), s)
         ctx.specs = specs
         ctx.counts = counts
         ctx.group = group
@@ -700,7 +766,7 @@ class _ConvBNMulti(torch.autograd.Function):
             buf[tot:].copy_(_counts_dev(ctx.counts, buf))
         lay = (_lib.BnLayer * n)()
         fins = (_lib.BnFin * n)()
-        keep, drs, dress = [], [], []
+        keep, drs, dress, red = [], [], [], []
         off = 0
         lib = _lib.load()
         for i in range(n):
@@ -709,9 +775,16 @@ class _ConvBNMulti(torch.autograd.Function):
             dy = as_act(dy) if dy is not None else torch.zeros_like(y)
             if not _bn_quad_ok(dy):  # e.g. a channel slice of a concatenation's gradient
                 dy = _aligned_copy(dy)
-            _, ra = act_of(r)
-            rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
-            part = _empty((2 * rows * cs[i],), r)
+            lz = spec.bn_out
+            pre = lz is not None and lz.part is not None and dys[i] is not None
+            if pre:  # partials from the consumer's data-gradient epilogue
+                part, rows = lz.part, lz.rows
+                lz.part = None
+            else:
+                _, ra = act_of(r)
+                rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
+                part = _empty((2 * rows * cs[i],), r)
+                red.append(i)
             dr = new_act(tuple(r.shape), r)
             dres, acc = None, 0
             if ctx.has_res[i] and need[1 + 6 * i + 5]:
@@ -735,9 +808,11 @@ class _ConvBNMulti(torch.autograd.Function):
             drs.append(dr)
             dress.append((dres, gret, bret))
             off += 2 * cs[i]
-        if prof.active():
-            prof.note(0, sum(4.0 * r.numel() * (3 if h_ else 2) for r, h_ in zip(rs, ctx.has_res)))
-        call("vae2_bn_multi_bwd_reduce", n, lay, s)
+        if red:
+            if prof.active():
+                prof.note(0, sum(4.0 * rs[i].numel() * (3 if ctx.has_res[i] else 2) for i in red))
+            call("vae2_bn_multi_bwd_reduce", len(red), (_lib.BnLayer * len(red))(*[lay[i] for i in red]),
+                 s)
         call("vae2_bn_multi_reduce", n, fins, 1, s)  # local sums + dgamma / dbeta
         if group is not None:  # SyncBN: global (sum g, sum g*xhat) for the input gradients
             from . import dist as vdist
@@ -794,10 +869,16 @@ def _bn_layer(x, a, o, dy, dres, save, gamma, part, sums_p, countp, count, relu,
 BN_BATCH = True  # False: conv_bn_multi runs its layers one by one (A/B and parity tests)
 
 
-def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=None):
+def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=None,
+                  bn_outs=None, bn_ins=None):
     """[conv_bn(xs[i], convs[i], bns[i], relu, residuals[i], ...)] for independent layers,
     their BatchNorm steps batched into shared launches (training mode; with SyncBN one
-    statistics exchange per direction for all of them)."""
+    statistics exchange per direction for all of them).
+
+    bn_outs[i] (a LazyBN, or None): layer i's BatchNorm output is consumed only by a conv
+    that takes it lazily -- the returned tensor is then the pre-BN conv output, to be
+    passed on with bn_ins[i] = that LazyBN to the consumer's conv_bn_multi call.  Where
+    the batched path does not run, the entry is set to None (the output is stored)."""
     n = len(xs)
     residuals = residuals if residuals is not None else [None] * n
     x_links = x_links if x_links is not None else [None] * n
@@ -807,9 +888,17 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
     for i in range(n):
         spec = ConvSpec(convs[i], bns[i], relus[i])
         spec.x_link, spec.res_link = x_links[i], res_links[i]
+        if bn_outs is not None:
+            spec.bn_out = bn_outs[i]
+        if bn_ins is not None:
+            spec.bn_in = bn_ins[i]
         specs.append(spec)
     if (not BN_BATCH or not all(sp.training for sp in specs) or
             not all(r is None or _bn_quad_ok(r) for r in residuals)):
+        if any(sp.bn_in is not None for sp in specs):
+            raise RuntimeError("a LazyBN input needs the batched training path")
+        if bn_outs is not None:
+            bn_outs[:] = [None] * n
         return [conv_bn(xs[i], convs[i], bns[i], relus[i], residuals[i], x_links[i],
                         res_links[i]) for i in range(n)]
     flat = []
