@@ -172,7 +172,9 @@ def test_direct_conv3x3_valu_remainder(shape):
     for c in (cout, cin):
         nr = c % 16
         if nr in (2, 4, 8) and c // 16 in (1, 2, 4):
-            assert any(k.endswith(f", {nr}>") and k.startswith("dconv3_kernel") for k in names), \
+            # dconv3_kernel<TM, TN, FLIP, BF, NR, BNX>
+            assert any(k.startswith("dconv3_kernel") and
+                       k[:-1].split(", ")[4:5] == [str(nr)] for k in names), \
                 (c, names)
     assert rel(nchw(yg), y_ref) < TOL
     assert rel(nchw(xg.grad), x.grad) < TOL
@@ -830,3 +832,70 @@ def test_up_avgpool_equals_upsample_then_pool(hw):
     assert rel(y1, y0) < 1e-6
     for a, b in zip(g1, g0):
         assert rel(a, b) < 1e-6
+
+
+GEMM1_SHAPES = [
+    # N, H, W, Cin, Cout, bias: 1x1 convs with >= 65536 pixels through the persistent
+    # LDS-weight GEMM (gemm1x1_kernel): the layer-1 expansions / reductions, a padded
+    # channel quad (70) with 2 N blocks of 5 tiles, a 3-block N (270)
+    (2, 128, 256, 64, 256, False),
+    (2, 128, 256, 256, 64, False),
+    (1, 256, 256, 70, 130, True),
+    (1, 128, 512, 36, 270, True),
+]
+
+
+@pytest.mark.parametrize("shape", GEMM1_SHAPES)
+def test_gemm1x1(shape):
+    """Forward (+ BN statistics through conv_bn), data gradient (+ beta = 1 accumulation
+    of a GradLink) and weight gradient against PyTorch fp32 on the CPU."""
+    from vae2 import ops, prof
+    torch.manual_seed(8)
+    n, h, w, cin, cout, bias = shape
+    conv = nn.Conv2d(cin, cout, 1, 1, 0, bias=bias)
+    x = torch.randn(n, cin, h, w, requires_grad=True)
+    y_ref = conv(x)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    cg = nn.Conv2d(cin, cout, 1, 1, 0, bias=bias).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+    with torch.no_grad():
+        xg.copy_(nhwc(x.detach()).to(DEV))
+    xg.requires_grad_(True)
+    _, xa = ops.act_of(xg)
+    assert prof.fwd_kernel_name(xa, (n, h, w, cout), 1, 1, 0).startswith("gemm1x1_kernel")
+    dyg = ops.new_act((n, h, w, cout), xg)
+    with torch.no_grad():
+        dyg.copy_(nhwc(gy).to(DEV))
+    yg = ops.conv(xg, cg)
+    yg.backward(dyg)
+    torch.cuda.synchronize()
+    assert rel(nchw(yg), y_ref) < TOL
+    assert rel(nchw(xg.grad), x.grad) < TOL
+    assert rel(cg.weight.grad, conv.weight.grad) < TOL
+    if bias:
+        assert rel(cg.bias.grad, conv.bias.grad) < TOL
+    # data gradient accumulated onto another consumer's (GradLink, beta = 1)
+    link = ops.GradLink(2)
+    other = torch.randn(n, h, w, cin)
+    link.buf = ops.new_act((n, h, w, cin), xg)
+    with torch.no_grad():
+        link.buf.copy_(other.to(DEV))
+    link.done = 1
+    x2 = xg.detach().clone().requires_grad_(True)
+    spec = ops.ConvSpec(cg)
+    spec.x_link = link
+    dx, _, _ = ops._conv_bwd(x2, cg.weight, cg.bias, dyg, spec, True, False, False)
+    torch.cuda.synchronize()
+    assert rel(dx.cpu(), nhwc(x.grad) + other) < TOL
+    # training BatchNorm after the conv: statistics from the persistent kernel's rows
+    if not bias:
+        bn = nn.BatchNorm2d(cout, momentum=0.01)
+        bg = nn.BatchNorm2d(cout, momentum=0.01).to(DEV)
+        ref = F.relu(bn(conv(x.detach())))
+        out = ops.conv_bn(xg.detach(), cg, bg, relu=True)
+        torch.cuda.synchronize()
+        assert rel(nchw(out), ref) < TOL
+        assert rel(bg.running_mean, bn.running_mean) < 1e-5
+        assert rel(bg.running_var, bn.running_var) < 1e-5

@@ -108,6 +108,28 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pa
 }
 
 #endif  // VAE2_PART(0)
+// 4 x 4 transpose across the 4 lanes of a lane quad (DPP quad_perm, no LDS): lane k's
+// v[e] becomes lane e's former v[k].  A 16x16 MFMA accumulator (lane (g, r) = column r,
+// rows 4g..4g+3) then has lane (g, 4Q + k) holding row 4g + k, columns 4Q..4Q+3.
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
+                                                            0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
+                                                            0x4E, 0xF, 0xF, true));
+}
+__device__ __forceinline__ void quad_transpose(f4& v, int k) {
+  const bool o = k & 1;
+  float a = dpp_xor1(o ? v[0] : v[1]), b = dpp_xor1(o ? v[2] : v[3]);
+  if (o) { v[0] = a; v[2] = b; } else { v[1] = a; v[3] = b; }
+  const bool h = k & 2;
+  a = dpp_xor2(h ? v[0] : v[2]);
+  b = dpp_xor2(h ? v[1] : v[3]);
+  if (h) { v[0] = a; v[1] = b; } else { v[2] = a; v[3] = b; }
+}
+
+
 // ------------------------------------------------------------ igemm ----
 struct IGemm {
   const float* a;  // gathered activation (NHWC)
@@ -125,6 +147,7 @@ struct IGemm {
   int y_ps, y_h, y_w, y_step, y_offh, y_offw;
   float beta;
   float* stats;  // [2][gridDim.x][n] or null
+  int vec_out;   // y 16-byte aligned, y_ps % 4 == 0, no statistics with beta != 0
   FastDiv hw_div, w_div;  // divide by g_h*g_w, g_w
   // Strided data gradient: one launch covers every stride-parity class of the input
   // pixels, class = blockIdx.z (gridDim.z == 1: the fields above are used as they are).
@@ -314,6 +337,57 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  if (p.vec_out && (KS == 1 || wave == 0)) {
+    // statistics in the MFMA layout (beta = 0 whenever they are requested), then each
+    // 16x16 tile transposed inside lane quads: one 16-byte store per lane and tile, and
+    // one output-pixel address per lane and row tile instead of four
+    const int k = r & 3, qc = 4 * (r >> 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (p.stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (mw + i * 16 + g * 4 + e >= M) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            if (n >= p.n) continue;
+            const float v = acc[i][j][e] + (p.bias ? p.bias[n] : 0.f);
+            csum[j] += v;
+            csq[j] += v * v;
+          }
+        }
+      }
+      const int m = mw + i * 16 + g * 4 + k;
+      const bool mok = m < M;
+      const int mm = mok ? m : 0;
+      const int gn = (int)p.hw_div.div((uint32_t)mm);
+      const int rem = mm - gn * p.g_h * p.g_w;
+      const int gi = (int)p.w_div.div((uint32_t)rem);
+      const int gj = rem - gi * p.g_w;
+      float* yrow = p.y + ((gn * p.y_h + gi * p.y_step + p.y_offh) * p.y_w +
+                           gj * p.y_step + p.y_offw) * p.y_ps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f4 v = acc[i][j];
+        quad_transpose(v, k);
+        const int n = n0 + j * 16 + qc;
+        if (!mok || n >= p.n) continue;
+        if (p.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
+        }
+        if (n + 3 < p.n) {
+          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          *reinterpret_cast<f4*>(yrow + n) = v;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n + q < p.n) yrow[n + q] = p.beta != 0.f ? v[q] + p.beta * yrow[n + q] : v[q];
+        }
+      }
+    }
+  } else
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -380,6 +454,190 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   }
 }
 
+
+// ----------------------------------------------------- 1x1 GEMM (persistent) ----
+// Large-M 1x1 / stride-1 convs (the layer-1 64 <-> 256 expansions and the 256 -> 64
+// reductions at full resolution) and their data gradients: Y[m][n] = sum_k X[m][k] W[n][k]
+// with W packed [Npad][K4] (mode 0; mode 1 for the data gradient is the same form).
+// The gather kernel gives each wave ONE 32-row tile with K = 64 (4 chunks): a full
+// load-latency prologue and an epilogue per 256 MFMAs, weights re-read per wave
+// (PMC: 52 % of wave cycles waiting, MFMA 36 % busy).  Here a workgroup stages its N block
+// of W (BN x K, zero past K) in LDS once; its 4 waves then stream row tiles of 16*TM pixels
+// (tile = blockIdx.x*4 + wave, + gridDim.x*4 per step) with the A fragments loaded two K
+// chunks ahead ACROSS tile boundaries, so the next tile's loads are in flight during this
+// tile's MFMAs and epilogue.  BN statistics accumulate over the wave's tiles: one partial
+// row per workgroup.
+struct Gemm1 {
+  const float* a;
+  int a_ps, a_c, a_c4, M;
+  const float* w;       // packed rows of a_c4 floats
+  int n;                // GEMM N (real)
+  const float* bias;
+  float* y;
+  int y_ps;
+  float beta;
+  float* stats;         // [2][gridDim.x][n] or null
+  uint32_t a_bytes, w_bytes;
+};
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
+  constexpr int BN = 16 * TN;
+  extern __shared__ __attribute__((aligned(16))) float bsh[];  // [BN][KL]
+  __shared__ float red[4][2][BN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int n0 = blockIdx.y * BN;
+  const int nch = (p.a_c4 + 15) >> 4;   // K chunks of 16
+  const int KL = nch * 16 + 4;          // LDS row stride (floats): conflict-free b128 reads
+  {
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
+    const int q4 = nch * 4;  // quads per staged row
+    for (int i = threadIdx.x; i < BN * q4; i += 256) {
+      const int nn = i / q4, q = i - nn * q4;
+      const bool ok = 4 * q < p.a_c4;  // (rows past the packed Npad: range check -> 0)
+      const f4 v = load4(wr, ok ? (uint32_t)((n0 + nn) * p.a_c4 + 4 * q) * 4u : kOOB);
+      *reinterpret_cast<f4*>(&bsh[nn * KL + 4 * q]) = v;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t ar = make_rsrc(p.a, p.a_bytes);
+  const int ntiles = (p.M + 16 * TM - 1) / (16 * TM);
+  const int t0 = blockIdx.x * 4 + wave, tstep = gridDim.x * 4;
+  const int iters = t0 < ntiles ? (ntiles - t0 + tstep - 1) / tstep : 0;
+  const int S = iters * nch;  // (tile, chunk) steps of this wave
+  const bool cpad = (p.a_c & 3) != 0;
+  float bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + j * 16 + r;
+    bv[j] = (p.bias && n < p.n) ? p.bias[n] : 0.f;
+  }
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  __syncthreads();  // W staged
+
+  auto load = [&](f4* fa, int st) {
+    const int it = st / nch, c = st - it * nch;
+    const int t = t0 + it * tstep;
+    const int q = 16 * c + 4 * g;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = t * 16 * TM + i * 16 + r;
+      const bool ok = st < S && m < p.M && q < p.a_c4;
+      fa[i] = load4(ar, ok ? (uint32_t)(m * p.a_ps + q) * 4u : kOOB);
+    }
+  };
+  auto step = [&](f4* fa, int st) {
+    const int it = st / nch, c = st - it * nch;
+    if (cpad && c == nch - 1) {  // channels past a_c in the last quad (a wider buffer's)
+      const int q = 16 * c + 4 * g;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        fa[i][1] = q + 1 < p.a_c ? fa[i][1] : 0.f;
+        fa[i][2] = q + 2 < p.a_c ? fa[i][2] : 0.f;
+        fa[i][3] = q + 3 < p.a_c ? fa[i][3] : 0.f;
+      }
+    }
+    f4 fb[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      fb[j] = *reinterpret_cast<const f4*>(&bsh[(j * 16 + r) * KL + 16 * c + 4 * g]);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+    if (c != nch - 1) return;
+    // the tile's epilogue, then a fresh accumulator.  BN partial sums in the MFMA layout
+    // (lane = column r, rows 4g..4g+3; statistics only with beta = 0), then each 16x16
+    // tile is transposed inside lane quads (DPP) so a lane holds 4 consecutive channels
+    // of one pixel: one 16-byte store instead of four 4-byte ones.
+    const int t = t0 + it * tstep;
+    const int k = r & 3, qc = 4 * (r >> 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = t * 16 * TM + i * 16 + 4 * g;
+      if (p.stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (mb + e < p.M && n0 + j * 16 + r < p.n) {
+              const float v = acc[i][j][e] + bv[j];
+              csum[j] += v;
+              csq[j] += v * v;
+            }
+          }
+        }
+      }
+      const int m = mb + k;
+      float* yrow = p.y + (int64_t)m * p.y_ps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f4 v = acc[i][j];
+        acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        quad_transpose(v, k);
+        const int n = n0 + j * 16 + qc;
+        if (m >= p.M || n >= p.n) continue;
+        if (p.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
+        }
+        if (n + 3 < p.n) {
+          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          *reinterpret_cast<f4*>(yrow + n) = v;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n + q < p.n) yrow[n + q] = p.beta != 0.f ? v[q] + p.beta * yrow[n + q] : v[q];
+        }
+      }
+    }
+  };
+  if (S > 0) {
+    f4 fa0[TM], fa1[TM];
+    load(fa0, 0);
+    for (int st = 0; st < S; st += 2) {
+      load(fa1, st + 1);
+      step(fa0, st);
+      load(fa0, st + 2);
+      if (st + 1 < S) step(fa1, st + 1);
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] += __shfl_xor(csum[j], 16, 64);
+      csum[j] += __shfl_xor(csum[j], 32, 64);
+      csq[j] += __shfl_xor(csq[j], 16, 64);
+      csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        red[wave][0][j * 16 + r] = csum[j];
+        red[wave][1][j * 16 + r] = csq[j];
+      }
+    }
+    __syncthreads();
+    const int rows = gridDim.x;
+    for (int c = threadIdx.x; c < BN; c += 256) {
+      if (n0 + c >= p.n) continue;
+      p.stats[blockIdx.x * p.n + n0 + c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      p.stats[(rows + blockIdx.x) * p.n + n0 + c] =
+          red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    }
+  }
+}
+
 // ------------------------------------------------------ direct 3x3 (LDS) ----
 // 3x3 / stride-1 / pad-1 convolutions (the HRNet branch convs) — forward, and the
 // data gradient with flipped taps and mode-1 weights.  A workgroup owns an output
@@ -415,6 +673,7 @@ struct DConv {
   const float* bx;
   int bx_ps, brelu;
   const float* bsave;
+  int vec_out;  // y 16-byte aligned, y_ps % 4 == 0, no statistics with beta != 0
 };
 
 constexpr int kDcBW = 32;     // tile columns
@@ -434,7 +693,10 @@ constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 8;
 // NR channels), v_fma_f32 chains over the same (tap, channel) K order the chunks walk,
 // with the remainder weights of the slab staged in LDS (broadcast reads).  The MFMA work
 // of an 18-channel layer halves (32 -> 16 columns), of a 36-channel one drops by 1/3.
-template <int TM, int TN, bool FLIP, bool BF, int NR = 0>
+// BNX (compile time, so the plain instances carry none of it): 1 = input BatchNorm in the
+// staging (DConv::isave, forward), 2 = producer BatchNorm backward partials in the
+// epilogue (DConv::bx, data gradient).
+template <int TM, int TN, bool FLIP, bool BF, int NR = 0, int BNX = 0>
 __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const int by,
                                             const int nrows, float* __restrict__ tile) {
   constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
@@ -535,7 +797,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const bool cpad = c + 4 > p.a_c;
     // input BatchNorm (FLIP = false only): this thread's channel quad's scale / shift
     f4 isc, ish;
-    if (!FLIP && p.isave) {
+    if (BNX == 1) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ch = c + k < p.a_c ? c + k : p.a_c - 1;
@@ -564,7 +826,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         for (int u = 0; u < SB; ++u) {
           const int pix = pix0 + u * pstride;
           if (pix >= LH * LW) break;
-          if (!FLIP && p.isave && okv[u]) {  // = bn_apply_body's arithmetic
+          if (BNX == 1 && okv[u]) {  // = bn_apply_body's arithmetic
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const float t = __builtin_fmaf(v[u][k], isc[k], ish[k]);
@@ -650,7 +912,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   float csum[TN], csq[TN];
   // producer BatchNorm backward partials (FLIP with bx): per-column mean, invstd, scale,
   // shift of that layer (= bn_bwd_reduce_body's arithmetic, element by element)
-  const bool bnp = FLIP && p.bx != nullptr;
+  constexpr bool bnp = BNX == 2;
   float bmn[TN], bis[TN], bsc[TN], bsh[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -661,6 +923,60 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       bsc[j] = p.bsave[2 * p.n + n]; bsh[j] = p.bsave[3 * p.n + n];
     }
   }
+  if (p.vec_out) {
+    // statistics in the MFMA layout (beta = 0 whenever they are requested), then each
+    // 16x16 tile transposed inside lane quads: one 16-byte store per lane and tile
+    const int k = r & 3, qc = 4 * (r >> 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int oh = oh0 + wave * (TM / 2) + (i >> 1);
+      if (p.stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
+          if (oh >= p.img_h || ow >= p.img_w) continue;
+          const int64_t pix = (int64_t)(img_base + oh) * p.img_w + ow;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            if (n >= p.n) continue;
+            const float v = acc[i][j][e] + (p.bias ? p.bias[n] : 0.f);
+            if (bnp) {
+              const float xv = p.bx[pix * p.bx_ps + n];
+              const float gv = (p.brelu && !(__builtin_fmaf(xv, bsc[j], bsh[j]) > 0.f)) ? 0.f : v;
+              csum[j] += gv;
+              csq[j] += gv * (xv - bmn[j]) * bis[j];
+            } else {
+              csum[j] += v;
+              csq[j] += v * v;
+            }
+          }
+        }
+      }
+      const int ow = ow0 + (i & 1) * 16 + g * 4 + k;
+      const bool pok = oh < p.img_h && ow < p.img_w;
+      float* yrow = p.y + ((int64_t)(img_base + (pok ? oh : 0)) * p.img_w + (pok ? ow : 0)) * p.y_ps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f4 v = acc[i][j];
+        quad_transpose(v, k);
+        const int n = n0 + j * 16 + qc;
+        if (!pok || n >= p.n) continue;
+        if (p.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
+        }
+        if (n + 3 < p.n) {
+          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          *reinterpret_cast<f4*>(yrow + n) = v;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n + q < p.n) yrow[n + q] = p.beta != 0.f ? v[q] + p.beta * yrow[n + q] : v[q];
+        }
+      }
+    }
+  } else
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int oh = oh0 + wave * (TM / 2) + (i >> 1);
@@ -762,10 +1078,11 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   }
 }
 
-template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0>
+template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0, int BNX = 0>
 __global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
+  static_assert(BNX == 0 || (!BF && (BNX == 1) != FLIP), "input BN: forward; partials: dgrad");
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  dconv3_body<TM, TN, FLIP, BF, NR>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
+  dconv3_body<TM, TN, FLIP, BF, NR, BNX>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
                                     tile);
 }
 
@@ -813,8 +1130,10 @@ int g_ksplit = 1;    // vae2_conv2d_set_algo bit 8 disables the K split (A/B tes
 int g_bf16 = 0;      // vae2_conv2d_set_mfma_bf16: bf16 MFMA operands (fp32 accumulate)
 int g_conv_algo = 0; // 0 auto, 1 gather kernel only, 2 direct wherever legal
 int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
+int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persistent 1x1 GEMM
+int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
 #else
-extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr;
+extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -858,7 +1177,42 @@ static bool vec_ok(const float* a, int ps) {
   return ((uintptr_t)a % 16 == 0) && (ps % 4 == 0);
 }
 
+
+// ---------------------------------------------------- 1x1 GEMM: host dispatch ----
+struct G1Tile {
+  int tn, nblk, grid_x;
+  size_t lds;
+};
+
+static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
+                       const float* a, G1Tile* out) {
+  if (!g_gemm1 || g_bf16 || g_conv_algo == 1) return false;
+  if (k != 1 || stride != 1 || pad != 0 || ad->h != yd->h || ad->w != yd->w) return false;
+  const int64_t M = act_pixels(yd);
+  const int N = (int)yd->c;
+  if (M < 65536 || N < 48 || !vec_ok(a, (int)ad->ps)) return false;
+  const int k4 = round_up((int)ad->c, 4);
+  const int tiles = (N + 15) / 16;
+  G1Tile t;
+  t.nblk = (tiles + 7) / 8;
+  t.tn = (tiles + t.nblk - 1) / t.nblk;
+  const int nch = (k4 + 15) / 16;
+  t.lds = (size_t)16 * t.tn * (nch * 16 + 4) * sizeof(float);
+  if (t.lds > 96 * 1024) return false;
+  const int per_cu = t.lds <= 40 * 1024 ? 3 : (t.lds <= 64 * 1024 ? 2 : 1);
+  const int64_t ntiles = ceil_div(M, 32);
+  int64_t gx = 256 * per_cu / t.nblk;
+  if (gx > ceil_div(ntiles, 4)) gx = ceil_div(ntiles, 4);
+  t.grid_x = (int)(gx < 1 ? 1 : gx);
+  if (out) *out = t;
+  return true;
+}
+
 int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls = 1);
+int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                 const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
+                 const G1Tile& t, hipStream_t s, const char* fn);
+
 
 #if VAE2_PART(1)
 template <int TM, bool VEC, int ROLE, int KS = 1>
@@ -919,6 +1273,7 @@ int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls) {
   for (int c = 0; c < ncls && ncls > 1; ++c)
     if (p.cls[c].nth * p.cls[c].ntw > max_taps) max_taps = p.cls[c].nth * p.cls[c].ntw;
   Tile t = pick_igemm_tile(M, p.n, max_taps, p.a_c4, ncls);
+  p.vec_out = g_vec_out && vec_ok(p.y, p.y_ps) && !(p.stats && p.beta != 0.f);
   p.hw_div = FastDiv((uint32_t)(p.g_h * p.g_w));
   p.w_div = FastDiv((uint32_t)p.g_w);
   dim3 grid((unsigned)ceil_div(M, igemm_rows_per_block(t)), (unsigned)t.nblk, (unsigned)ncls);
@@ -932,6 +1287,7 @@ int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls) {
   }
   return check_launch(fn);
 }
+
 
 #endif  // VAE2_PART(1)
 
@@ -1574,6 +1930,30 @@ static uint32_t act_bytes(const vae2_act* d) {
   return (uint32_t)(last * 4);
 }
 
+#if VAE2_PART(1)
+int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                 const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
+                 const G1Tile& t, hipStream_t s, const char* fn) {
+  // (16-byte stores of whole channel quads; statistics are of the fresh output only)
+  if (!vec_ok(y, (int)yd->ps) || (stats && beta != 0.f)) return -1;
+  Gemm1 p{};
+  p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
+  p.M = (int)act_pixels(yd);
+  p.w = wp; p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
+  p.stats = stats; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
+  const dim3 grid((unsigned)t.grid_x, (unsigned)t.nblk);
+  switch (t.tn) {
+#define CASE(T) \
+  case T: VAE2_LAUNCH((gemm1x1_kernel<2, T>), grid, dim3(256), t.lds, s, p); break;
+    CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default: return fail(fn, "gemm1x1: unsupported N block");
+  }
+  return check_launch(fn);
+}
+
+#endif  // VAE2_PART(1)
+
 }  // namespace vae2
 
 using namespace vae2;
@@ -1657,6 +2037,22 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
 template <int TM, bool FLIP>
 static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s,
                             int nr = 0) {
+  if (p.isave || p.bx) {  // fused BatchNorm (fp32 operands): forward input / dgrad partials
+    constexpr int X = FLIP ? 2 : 1;
+    if (nr) {
+      if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2, X>), grid, dim3(256), shm, s, p);
+      else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4, X>), grid, dim3(256), shm, s, p);
+      else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8, X>), grid, dim3(256), shm, s, p);
+      return;
+    }
+    switch (tn) {
+#define CASE(T) \
+  case T: VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, false, 0, X>), grid, dim3(256), shm, s, p); break;
+      CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+    }
+    return;
+  }
   if (nr) {  // fp32 operands (pick_dtile)
     if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2>), grid, dim3(256), shm, s, p);
     else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4>), grid, dim3(256), shm, s, p);
@@ -1686,6 +2082,7 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
   p.w = wp; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
   p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
   p.stats = stats;
+  p.vec_out = g_vec_out && vec_ok(y, (int)yd->ps) && !(stats && beta != 0.f);
   return p;
 }
 
@@ -1722,6 +2119,7 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.stats = stats;
   p.isave = bn.isave; p.irelu = bn.irelu;
   p.bx = bn.bx; p.bx_ps = bn.bx_ps; p.brelu = bn.brelu; p.bsave = bn.bsave;
+  p.vec_out = g_vec_out && vec_ok(y, (int)yd->ps) && !(stats && beta != 0.f);
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
   const size_t shm = dconv_shm(d);
   if (d.tm == 4) {
@@ -1952,13 +2350,16 @@ int vae2_wgrad_flush(void* stream) {
 
 #if VAE2_PART(0)
 int vae2_conv2d_set_algo(int algo) {
-  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) + (g_dconv_nr ? 0 : 16);
+  const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) +
+                   (g_dconv_nr ? 0 : 16) + (g_gemm1 ? 0 : 32) + (g_vec_out ? 0 : 64);
   const int a = algo & 7;
-  if (algo >= 0 && algo <= 31 && a <= 6 && a != 3) {
+  if (algo >= 0 && algo <= 127 && a <= 6 && a != 3) {
     g_conv_algo = a & 3;
     g_wide_tiles = a < 4;
     g_ksplit = !(algo & 8);
     g_dconv_nr = !(algo & 16);
+    g_gemm1 = !(algo & 32);
+    g_vec_out = !(algo & 64);
   }
   return prev;
 }
@@ -1967,6 +2368,8 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
                                    int k, int stride, int pad) {
   if (!act_ok(xd) || !act_ok(yd)) return 0;
   if (dconv_use(xd, yd, k, stride, pad, x)) return dconv_rows(xd, yd);
+  G1Tile g1;
+  if (gemm1_pick(xd, yd, k, stride, pad, x, &g1)) return g1.grid_x;
   return igemm_rows(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4));
 }
 
@@ -1979,6 +2382,11 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
       snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false, false, %d>", d.tm, d.tn, d.nr);
     else
       snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false>", d.tm, d.tn);
+    return 0;
+  }
+  G1Tile g1;
+  if (gemm1_pick(xd, yd, k, stride, pad, (const float*)16, &g1)) {
+    snprintf(buf, (size_t)len, "gemm1x1_kernel<2, %d>", g1.tn);
     return 0;
   }
   Tile t = pick_igemm_tile(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4), 1);
@@ -2000,6 +2408,14 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
   if (dconv_use(xd, yd, k, stride, pad, x)) {
     return launch_dconv(x, xd, wp, (uint32_t)(vae2_conv2d_packed_size(yd->c, xd->c, k, 0) * 4),
                         bias, y, yd, beta, stats, false, as_stream(stream), fn);
+  }
+  G1Tile g1;
+  if (gemm1_pick(xd, yd, k, stride, pad, x, &g1)) {
+    const int rc = launch_gemm1(x, xd, wp,
+                                (uint32_t)(vae2_conv2d_packed_size(yd->c, xd->c, k, 0) * 4),
+                                bias, y, yd, beta, stats, g1, as_stream(stream), fn);
+    if (rc != -1) return rc;
+    VAE2_REQUIRE(stats == nullptr, fn, "BN statistics need a 16-byte aligned output here");
   }
   IGemm p{};
   p.a = x; p.a_ps = (int)xd->ps; p.a_c = (int)xd->c; p.a_c4 = round_up((int)xd->c, 4);
@@ -2023,7 +2439,7 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
 int vae2_conv2d_bnin_ok(const float* x, const vae2_act* xd, const vae2_act* yd, int k,
                         int stride, int pad) {
   if (!x || !conv_shapes_ok(xd, yd, k, stride, pad) || !fits32(xd) || !fits32(yd)) return 0;
-  return dconv_use(xd, yd, k, stride, pad, x) && g_conv_algo != 1 &&
+  return !g_bf16 && dconv_use(xd, yd, k, stride, pad, x) && g_conv_algo != 1 &&
          wgrad3_shape_ok(xd, yd, k, stride, pad) && vec_ok(x, (int)xd->ps);
 }
 
@@ -2046,7 +2462,7 @@ int64_t vae2_conv2d_bwd_data_bnpart_rows(const float* dy, const vae2_act* dyd,
                                          const vae2_act* dxd, int k, int stride, int pad) {
   if (!dy || !conv_shapes_ok(dxd, dyd, k, stride, pad) || !fits32(dxd) || !fits32(dyd))
     return 0;
-  return dconv_use(dyd, dxd, k, stride, pad, dy) ? dconv_rows(dyd, dxd) : 0;
+  return !g_bf16 && dconv_use(dyd, dxd, k, stride, pad, dy) ? dconv_rows(dyd, dxd) : 0;
 }
 
 int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const float* wp,
@@ -2080,6 +2496,13 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
   if (dconv_use(dyd, dxd, k, stride, pad, dy))
     return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
                         nullptr, dx, dxd, beta, nullptr, true, as_stream(stream), fn);
+  G1Tile g1;
+  if (gemm1_pick(dyd, dxd, k, stride, pad, dy, &g1)) {
+    const int rc = launch_gemm1(dy, dyd, wp,
+                                (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
+                                nullptr, dx, dxd, beta, nullptr, g1, as_stream(stream), fn);
+    if (rc != -1) return rc;
+  }
   // Stride-parity classes (ph, pw) of the input pixels: input row ih = stride*i + ph
   // receives from output row oh = (ih + pad - kh)/stride for every kh with
   // (ph + pad - kh) % stride == 0.  All classes run in one launch (class = blockIdx.z);
