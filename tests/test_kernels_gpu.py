@@ -899,3 +899,38 @@ def test_gemm1x1(shape):
         assert rel(nchw(out), ref) < TOL
         assert rel(bg.running_mean, bn.running_mean) < 1e-5
         assert rel(bg.running_var, bn.running_var) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [
+    # N, H, W, Cin, Cout, k, stride: gather weight gradients with 16-byte channel-quad
+    # operand loads (aligned NHWC: wgrad_kernel<..., V4>), incl. padded quads (18, 5, 7)
+    (2, 32, 64, 18, 36, 3, 2),
+    (2, 16, 32, 36, 72, 3, 2),
+    (2, 64, 64, 64, 64, 1, 1),
+    (1, 9, 13, 5, 7, 3, 2),
+    (2, 12, 20, 256, 18, 3, 2),
+])
+def test_wgrad_quad_loads(shape):
+    from vae2 import ops
+    torch.manual_seed(9)
+    n, h, w, cin, cout, k, s = shape
+    conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=False)
+    x = torch.randn(n, cin, h, w)
+    y_ref = conv(x)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    cg = nn.Conv2d(cin, cout, k, s, k // 2, bias=False).to(DEV)
+    cg.load_state_dict(conv.state_dict())
+    xg = ops.new_act((n, h, w, cin), torch.empty(1, device=DEV))
+    with torch.no_grad():
+        xg.copy_(nhwc(x).to(DEV))
+    oh, ow = y_ref.shape[2:]
+    dyg = ops.new_act((n, oh, ow, cout), xg)
+    with torch.no_grad():
+        dyg.copy_(nhwc(gy).to(DEV))
+    spec = ops.ConvSpec(cg)
+    _, wret, _ = ops._conv_bwd(xg, cg.weight, None, dyg, spec, False, True, False)
+    ops.flush_wgrad()
+    torch.cuda.synchronize()
+    got = cg.weight.grad if wret is None else wret
+    assert rel(got, conv.weight.grad) < TOL

@@ -1314,7 +1314,12 @@ struct WGrad {
   FastDiv ohw_div, ow_div, cin4_div;
 };
 
-template <int TM, int TN, bool BF = false>
+// V4 (16-byte aligned NHWC operands): lane (g, 4Q + k) loads ONE 16-byte channel quad
+// of pixel 4g + k per operand tile -- dY[px][co 4Q..4Q+3], X[src(px)][ci 4Q..4Q+3] -- and
+// a 4x4 transpose inside its lane quad (quad_transpose, DPP) turns those into the MFMA
+// fragments (4 pixels of one co / ci), instead of four 4-byte loads with four pixel
+// address computations per operand tile.
+template <int TM, int TN, bool BF = false, bool V4 = false>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
   extern __shared__ __attribute__((aligned(16))) float wred[];  // [3][TM*TN*4][64]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1335,9 +1340,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
   }
   int bkh[TN], bkw[TN], boff[TN];
   bool bok[TN];
+  const int kq = r & 3;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = col0 + j * 16 + r;
+    const int col = col0 + j * 16 + (V4 ? 4 * (r >> 2) : r);  // (V4: the lane's channel quad)
     const int t = (int)p.cin4_div.div((uint32_t)col);
     const int ci = col - t * p.cin4;
     bkh[j] = t / p.k;
@@ -1355,6 +1361,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
   // chunk loads (pixels past pend load 0), double-buffered in registers: the next
   // chunk's loads are in flight across this chunk's MFMAs
   auto load = [&](int pc, f4* fa, f4* fb) {
+    if constexpr (V4) {
+      const int pix = pc + 4 * g + kq;
+      const bool pv = pix < pend;
+      const int pp = pv ? pix : pbeg;
+      const int n = (int)p.ohw_div.div((uint32_t)pp);
+      const int rem = pp - n * ohw;
+      const int oh = (int)p.ow_div.div((uint32_t)rem);
+      const int ow = rem - oh * p.o_w;
+      const uint32_t drow = (uint32_t)(pp * p.dy_ps);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int co = co0 + i * 16 + 4 * (r >> 2);
+        fa[i] = load4(dr, (pv && co < p.cout) ? (drow + co) * 4u : kOOB);
+      }
+      const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
+      const int xc = ((n * p.x_h + ih0) * p.x_w + iw0) * p.x_ps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int ih = ih0 + bkh[j], iw = iw0 + bkw[j];
+        const bool ok = pv && bok[j] && (unsigned)ih < (unsigned)p.x_h &&
+                        (unsigned)iw < (unsigned)p.x_w;
+        fb[j] = load4(xr, ok ? (uint32_t)(xc + boff[j]) * 4u : kOOB);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int pix = pc + 4 * g + s;
@@ -1379,7 +1410,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
       }
     }
   };
-  auto mma = [&](const f4* fa, const f4* fb) {
+  auto quads = [&](f4* fa, f4* fb) {  // V4: quad loads -> fragments (after they landed)
+    if constexpr (V4) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) quad_transpose(fa[i], kq);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) quad_transpose(fb[j], kq);
+    }
+  };
+  auto mma = [&](f4* fa, f4* fb) {
+    quads(fa, fb);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -1404,6 +1444,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WGrad p) {
       load(pc + 64, fa1, fb1);
       for (; pc < pend; pc += 128) {
         bf16x8 A[TM], B[TN];
+        quads(fa0, fb0);
+        quads(fa1, fb1);
 #pragma unroll
         for (int i = 0; i < TM; ++i) A[i] = pack_bf16(fa0[i], fa1[i]);
 #pragma unroll
@@ -1881,27 +1923,25 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
 }
 
 #if VAE2_PART(3)
-template <int TM>
-static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
+template <int TM, bool V4>
+static void launch_wgrad_tn_v(const WGrad& p, int tn, dim3 grid, hipStream_t s) {
   const size_t lds = (size_t)3 * TM * 4 * 4 * 64 * sizeof(float) / 4 * tn;  // 3 waves x NV x 64
   switch (tn) {
-    case 1:
-      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 1, true>), grid, dim3(256), lds, s, p);
-      else VAE2_LAUNCH((wgrad_kernel<TM, 1>), grid, dim3(256), lds, s, p);
-      break;
-    case 2:
-      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 2, true>), grid, dim3(256), lds, s, p);
-      else VAE2_LAUNCH((wgrad_kernel<TM, 2>), grid, dim3(256), lds, s, p);
-      break;
-    case 3:
-      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 3, true>), grid, dim3(256), lds, s, p);
-      else VAE2_LAUNCH((wgrad_kernel<TM, 3>), grid, dim3(256), lds, s, p);
-      break;
-    default:
-      if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, 4, true>), grid, dim3(256), lds, s, p);
-      else VAE2_LAUNCH((wgrad_kernel<TM, 4>), grid, dim3(256), lds, s, p);
-      break;
+#define CASE(T) \
+  case T: \
+    if (g_bf16) VAE2_LAUNCH((wgrad_kernel<TM, T, true, V4>), grid, dim3(256), lds, s, p); \
+    else VAE2_LAUNCH((wgrad_kernel<TM, T, false, V4>), grid, dim3(256), lds, s, p); \
+    break;
+    CASE(1) CASE(2) CASE(3)
+    default: CASE(4)
+#undef CASE
   }
+}
+
+template <int TM>
+static void launch_wgrad_tn(const WGrad& p, int tn, dim3 grid, hipStream_t s, bool v4) {
+  if (v4) launch_wgrad_tn_v<TM, true>(p, tn, grid, s);
+  else launch_wgrad_tn_v<TM, false>(p, tn, grid, s);
 }
 
 #endif  // VAE2_PART(3)
@@ -2731,11 +2771,13 @@ static int bwd_weight_impl(const float* x, const vae2_act* xd, const float* dy,
   p.ow_div = FastDiv((uint32_t)dyd->w);
   p.cin4_div = FastDiv((uint32_t)cin4);
   dim3 grid(t.gx, t.gy, (unsigned)t.splits);
+  // 16-byte channel-quad operand loads (quad-transposed into fragments)
+  const bool v4 = g_vec_out && vec_ok(x, (int)xd->ps) && vec_ok(dy, (int)dyd->ps);
   switch (t.tm) {
-    case 1: launch_wgrad_tn<1>(p, t.tn, grid, s); break;
-    case 2: launch_wgrad_tn<2>(p, t.tn, grid, s); break;
-    case 3: launch_wgrad_tn<3>(p, t.tn, grid, s); break;
-    default: launch_wgrad_tn<4>(p, t.tn, grid, s); break;
+    case 1: launch_wgrad_tn<1>(p, t.tn, grid, s, v4); break;
+    case 2: launch_wgrad_tn<2>(p, t.tn, grid, s, v4); break;
+    case 3: launch_wgrad_tn<3>(p, t.tn, grid, s, v4); break;
+    default: launch_wgrad_tn<4>(p, t.tn, grid, s, v4); break;
   }
   int rc = check_launch(fn);
   if (rc) return rc;
