@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--lazy-bn", choices=("on", "off"), default="on",
                     help="BasicBlock bn1 normalised inside conv2's staging, never stored "
                          "(vae2.ops.LazyBN; A/B)")
+    ap.add_argument("--conv-algo", type=int, default=None,
+                    help="vae2_conv2d_set_algo bits (A/B of kernel choices; default: auto)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
     ap.add_argument("--full-step", action="store_true",
@@ -237,6 +239,9 @@ def main():
     if args.conv_grouping == "on":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_grouping(1)
+    if args.conv_algo is not None:
+        from vae2 import _lib
+        _lib.load().vae2_conv2d_set_algo(args.conv_algo)
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False

@@ -367,6 +367,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       const int gj = rem - gi * p.g_w;
       float* yrow = p.y + ((gn * p.y_h + gi * p.y_step + p.y_offh) * p.y_w +
                            gj * p.y_step + p.y_offw) * p.y_ps;
+      // beta: the row tile's old output quads all loaded before any store (one round trip
+      // per row tile instead of one per quad: loads cannot pass the stores to y)
+      f4 yold[TN];
+      if (p.beta != 0.f) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + j * 16 + qc;
+          yold[j] = (mok && n + 3 < p.n) ? *reinterpret_cast<const f4*>(yrow + n)
+                                         : f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         f4 v = acc[i][j];
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
           for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
         }
         if (n + 3 < p.n) {
-          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          if (p.beta != 0.f) v += p.beta * yold[j];
           *reinterpret_cast<f4*>(yrow + n) = v;
         } else {
 #pragma unroll
@@ -580,6 +591,15 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
       }
       const int m = mb + k;
       float* yrow = p.y + (int64_t)m * p.y_ps;
+      f4 yold[TN];  // beta: loaded before any store (one round trip per row tile)
+      if (p.beta != 0.f) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + j * 16 + qc;
+          yold[j] = (m < p.M && n + 3 < p.n) ? *reinterpret_cast<const f4*>(yrow + n)
+                                             : f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         f4 v = acc[i][j];
@@ -592,7 +612,7 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
           for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
         }
         if (n + 3 < p.n) {
-          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          if (p.beta != 0.f) v += p.beta * yold[j];
           *reinterpret_cast<f4*>(yrow + n) = v;
         } else {
 #pragma unroll
@@ -927,6 +947,28 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     // statistics in the MFMA layout (beta = 0 whenever they are requested), then each
     // 16x16 tile transposed inside lane quads: one 16-byte store per lane and tile
     const int k = r & 3, qc = 4 * (r >> 2);
+    // beta (a data gradient summed onto a GradLink buffer): every old output quad of the
+    // tile loaded before any store (loads cannot pass the stores to y: one round trip
+    // instead of one per quad)
+    constexpr bool PFA = TM * TN <= 8;
+    f4 yold[PFA ? TM : 1][TN];
+    auto yrow_of = [&](int i) {
+      const int oh = oh0 + wave * (TM / 2) + (i >> 1), ow = ow0 + (i & 1) * 16 + g * 4 + k;
+      const bool pok = oh < p.img_h && ow < p.img_w;
+      return pok ? p.y + ((int64_t)(img_base + oh) * p.img_w + ow) * p.y_ps : nullptr;
+    };
+    auto prefetch = [&](int i, f4* yo) {
+      const float* yr = yrow_of(i);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 16 + qc;
+        yo[j] = (yr && n + 3 < p.n) ? *reinterpret_cast<const f4*>(yr + n) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    if (PFA && p.beta != 0.f) {
+#pragma unroll
+      for (int i = 0; i < (PFA ? TM : 1); ++i) prefetch(i, yold[i]);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int oh = oh0 + wave * (TM / 2) + (i >> 1);
@@ -953,9 +995,10 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
           }
         }
       }
-      const int ow = ow0 + (i & 1) * 16 + g * 4 + k;
-      const bool pok = oh < p.img_h && ow < p.img_w;
-      float* yrow = p.y + ((int64_t)(img_base + (pok ? oh : 0)) * p.img_w + (pok ? ow : 0)) * p.y_ps;
+      float* yrow = yrow_of(i);
+      const bool pok = yrow != nullptr;
+      f4 yrt[PFA ? 1 : TN];
+      if (!PFA && p.beta != 0.f) prefetch(i, yrt);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         f4 v = acc[i][j];
@@ -967,7 +1010,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
           for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
         }
         if (n + 3 < p.n) {
-          if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f4*>(yrow + n);
+          if (p.beta != 0.f) v += p.beta * (PFA ? yold[PFA ? i : 0][j] : yrt[PFA ? 0 : j]);
           *reinterpret_cast<f4*>(yrow + n) = v;
         } else {
 #pragma unroll
@@ -1132,8 +1175,10 @@ int g_conv_algo = 0; // 0 auto, 1 gather kernel only, 2 direct wherever legal
 int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
 int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persistent 1x1 GEMM
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
+int g_dconv_nr_wide = 0;  // vae2_conv2d_set_algo bit 128: the 36 / 72-channel remainder forms
 #else
-extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out;
+extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
+    g_dconv_nr_wide;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2025,7 +2070,7 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   //  MFMA tiles; algo 2 takes all three, for the tests)
   if (remainder && g_dconv_nr && !g_bf16 &&
       ((tn == 1 && nr == 2) ||
-       (g_conv_algo == 2 && ((tn == 2 && nr == 4) || (tn == 4 && nr == 8))))) {
+       ((g_conv_algo == 2 || g_dconv_nr_wide) && ((tn == 2 && nr == 4) || (tn == 4 && nr == 8))))) {
     d.tn = tn;
     d.nr = nr;
     d.nblk = 1;
@@ -2391,9 +2436,11 @@ int vae2_wgrad_flush(void* stream) {
 #if VAE2_PART(0)
 int vae2_conv2d_set_algo(int algo) {
   const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) +
-                   (g_dconv_nr ? 0 : 16) + (g_gemm1 ? 0 : 32) + (g_vec_out ? 0 : 64);
+                   (g_dconv_nr ? 0 : 16) + (g_gemm1 ? 0 : 32) + (g_vec_out ? 0 : 64) +
+                   (g_dconv_nr_wide ? 128 : 0);
   const int a = algo & 7;
-  if (algo >= 0 && algo <= 127 && a <= 6 && a != 3) {
+  if (algo >= 0 && algo <= 255 && a <= 6 && a != 3) {
+    g_dconv_nr_wide = (algo & 128) ? 1 : 0;
     g_conv_algo = a & 3;
     g_wide_tiles = a < 4;
     g_ksplit = !(algo & 8);
