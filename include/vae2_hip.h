@@ -58,7 +58,10 @@ int64_t vae2_conv2d_fwd_stats_rows(const float* x, const vae2_act* xd, const vae
  * implicit-GEMM kernel only, 2 = the LDS-tiled direct 3x3 kernel wherever legal
  * (k = 3, stride 1, pad 1, 16-byte aligned input with ps % 4 == 0); + 4 also
  * disables the wide-N tiles of 1x1 convs, + 8 the in-workgroup K split of the
- * implicit-GEMM kernel for layers with few row tiles.  Returns the previous setting.
+ * implicit-GEMM kernel for layers with few row tiles, + 16 the VALU-remainder channels of
+ * the direct 3x3 kernels (18 = 16 + 2 ...), + 32 the persistent 1x1 GEMM, + 64 the
+ * quad-transposed 16-byte epilogue stores / operand loads, + 128 the 32 + 4 and 64 + 8
+ * remainder forms in auto mode.  Returns the previous setting.
  * Process-wide; set it before building stats buffers.                           */
 int vae2_conv2d_set_algo(int algo);
 /* MFMA operand precision of every conv kernel (forward, data and weight gradient):

@@ -1175,7 +1175,7 @@ int g_conv_algo = 0; // 0 auto, 1 gather kernel only, 2 direct wherever legal
 int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU remainder
 int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persistent 1x1 GEMM
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
-int g_dconv_nr_wide = 0;  // vae2_conv2d_set_algo bit 128: the 36 / 72-channel remainder forms
+int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide;
@@ -2066,8 +2066,10 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   d.tn = t.tn;
   d.nblk = t.nblk;
   const int N = (int)yd->c, tn = N / 16, nr = N % 16;
-  // (auto: 16 + 2 only — the 36 / 72-channel forms measured slower than their padded
-  //  MFMA tiles; algo 2 takes all three, for the tests)
+  // (auto: all three where the single N block still fills the chip twice -- in the
+  //  concurrent training step the 32 + 4 form is 0.4 % faster than the padded 48-column
+  //  tiles; set_algo bit 128 restricts auto to 16 + 2; algo 2 takes all three wherever
+  //  legal, for the tests)
   if (remainder && g_dconv_nr && !g_bf16 &&
       ((tn == 1 && nr == 2) ||
        ((g_conv_algo == 2 || g_dconv_nr_wide) && ((tn == 2 && nr == 4) || (tn == 4 && nr == 8))))) {
@@ -2437,10 +2439,10 @@ int vae2_wgrad_flush(void* stream) {
 int vae2_conv2d_set_algo(int algo) {
   const int prev = g_conv_algo + (g_wide_tiles ? 0 : 4) + (g_ksplit ? 0 : 8) +
                    (g_dconv_nr ? 0 : 16) + (g_gemm1 ? 0 : 32) + (g_vec_out ? 0 : 64) +
-                   (g_dconv_nr_wide ? 128 : 0);
+                   (g_dconv_nr_wide ? 0 : 128);
   const int a = algo & 7;
   if (algo >= 0 && algo <= 255 && a <= 6 && a != 3) {
-    g_dconv_nr_wide = (algo & 128) ? 1 : 0;
+    g_dconv_nr_wide = (algo & 128) ? 0 : 1;
     g_conv_algo = a & 3;
     g_wide_tiles = a < 4;
     g_ksplit = !(algo & 8);
