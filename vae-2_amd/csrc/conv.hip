@@ -1958,6 +1958,7 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   int64_t tiles = (int64_t)t.gx * t.gy;
   // ~1024 workgroups (4 waves each), at least 256 pixels (4 chunks per wave) each: small
   // layers get enough workgroups in flight to hide the load latency
+  // (512 / 256 measured 0.5 / 1.2 % slower in the step)
   int64_t want = ceil_div(1024, tiles);
   int64_t maxs = ceil_div(P, 256);
   int64_t s = want < maxs ? want : maxs;
@@ -2283,6 +2284,11 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
     t.tps = (int)ceil_div(t.ntiles, w2);
     if (t.tps < 2) t.tps = 2;
   }
+  // at least 2 tiles per split: half the partial dW slabs (written here, read back by the
+  // end-of-backward reductions) -- 36 -> 36 at 64x128 wrote 24 MB of slabs per launch,
+  // 2.5x its dY.  In the concurrent training step: 814.7 -> 822.6 frames/s (A/B, same
+  // box); 4 tiles per split: 789
+  if (t.tps < 2) t.tps = 2;
   t.splits = (int)ceil_div(t.ntiles, t.tps);
   return t;
 }
