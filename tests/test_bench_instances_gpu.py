@@ -280,7 +280,8 @@ def test_conv_instances_at_bench_geometry(bench_step):
         for key in keys:
             {"fwd": _replay_fwd, "dgrad": _replay_dgrad, "wgrad": _replay_wgrad}[key[0]](key, lib)
     got = _kernels(rec.calls, CONV_ABI)
-    want = {k for k in want if _family(k) in ("conv_fwd", "conv_dgrad", "conv_wgrad")}
+    want = {k for k in want if _family(k) in ("conv_fwd", "conv_dgrad", "conv_wgrad",
+                                             "conv_1x1")}
     missing = sorted(want - got)
     assert not missing, missing
     print(f"{len(keys)} distinct conv calls, {len(want)} kernel instances replayed")

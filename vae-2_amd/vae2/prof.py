@@ -29,6 +29,7 @@ FAMILIES = (
     ("conv_fwd", r"dconv3_(group_)?kernel<\d+, \d+, false|igemm_kernel<\d+, \d+, \w+, 0"),
     ("conv_dgrad", r"dconv3_(group_)?kernel<\d+, \d+, true|igemm_kernel<\d+, \d+, \w+, [12]"),
     ("conv_wgrad", r"wgrad"),
+    ("conv_1x1", r"gemm1x1"),  # persistent 1x1 GEMM: forward and data gradient
     ("batchnorm", r"bn_|reduce_then|chan_partials|partials_reduce"),
     ("heads", r"upsum|head_|up_adj"),
     ("fuse_resample", r"upsample|fuse_sum|relu_bwd|copy_act|tile_kernel|spatial_|codemap"),
