@@ -66,9 +66,10 @@ def parse():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--clip-length", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=None,
-                    help="clips per CPU step (default: the GPU's clips per step)")
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-batch", type=int, default=2,
+                    help="clips per CPU step (a bounded sample: 1 warm-up + --cpu-steps timed "
+                         "steps at 8 clips would take ~2 min of the driver's run)")
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--profile-json", default=None,
@@ -198,8 +199,7 @@ def cpu_baseline(args, config, gpu_batch):
         terms["loss_all"].backward()
         opt.step()
 
-    if args.cpu_steps > 1:
-        step()  # warm-up (the default single timed step has none: ~20 s at 8 clips)
+    step()  # warm-up (allocator, oneDNN primitive caches)
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
         step()
@@ -209,7 +209,7 @@ def cpu_baseline(args, config, gpu_batch):
             "sample": f"oracle/ref_cpu.py ELBO step fwd+bwd+torch Adam (the reference's ATen "
                       f"ops), HRNet-W18-small-v2 {H}x{W}, {B} clips x {3 * L} frames per step "
                       f"(the GPU runs {gpu_batch} clips/step), fp32, "
-                      f"{'1 warm-up + ' if args.cpu_steps > 1 else ''}{args.cpu_steps} timed "
+                      f"1 warm-up + {args.cpu_steps} timed "
                       f"step(s) ({dt:.2f} s/step), torch threads={cores} = the box's CPU "
                       f"share for one GPU (OMP_NUM_THREADS; {aff} in the affinity mask), "
                       f"CPU: {cpu_model()}"}
@@ -359,6 +359,11 @@ def main():
                                          "HBM, fp32 BN / loss / Adam)" if args.dtype == "bf16"
                                          else "fp32")},
             "last_loss": last_loss,
+            # also clips/s and predicted frames/s (2L of the 3L frames a clip
+            # carries are predicted: x2t_hat and x3t_hat; xt_hat reconstructs the context)
+            "clips_per_s": round(world * B * args.steps / elapsed, 3),
+            "predicted_frames_per_s": round(world * B * 2 * L * args.steps / elapsed, 2),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         }
         if profiler is not None:
             n = args.roofline_steps
@@ -388,6 +393,20 @@ def main():
             if ref_gf is not None and L == 3 and not full:
                 roof["step_frac_ref_flops"] = round(
                     B * ref_gf / ms / prof.MFMA_PEAK_TF, 4)
+            # the north star's target: the encoder / decoder conv stack as a whole -- every conv
+            # family's algorithmic FLOPs over its summed kernel time, against the MFMA peak
+            conv = [r for r in summ["families"]
+                    if r["name"] in ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_1x1")]
+            c_ms = sum(r["ms_per_step"] for r in conv)
+            c_gf = sum(r.get("gflop_per_step", 0.0) for r in conv)
+            if c_ms > 0:
+                c_tf = c_gf / c_ms
+                roof["conv_stack"] = {"families": [r["name"] for r in conv],
+                                      "gflop_per_step": round(c_gf, 1),
+                                      "kernel_ms_per_step": round(c_ms, 3),
+                                      "achieved": round(c_tf, 2), "peak": prof.MFMA_PEAK_TF,
+                                      "unit": "TFLOP/s", "bound": "mfma",
+                                      "frac": round(c_tf / prof.MFMA_PEAK_TF, 4)}
             roof["measured"] = (f"{n} eager steps after the timed region, every C-ABI call "
                                 "timed with HIP events on its stream, isolated from side "
                                 "streams")

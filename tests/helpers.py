@@ -86,6 +86,13 @@ def rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+def rel_nz(a, b):
+    """rel(a, b) for a reference that must not be all zero (a lost gradient on both sides
+    would otherwise compare equal)."""
+    assert b is not None and float(b.detach().double().norm()) > 0, "reference is all zero"
+    return rel(a, b)
+
+
 def max_rel(a, b):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()

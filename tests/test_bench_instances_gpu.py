@@ -36,7 +36,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 B, H, W = 8, 128, 256
 CONV_ABI = ("vae2_conv2d_fwd", "vae2_conv2d_bwd_data", "vae2_conv2d_bwd_weight",
-            "vae2_conv2d_bwd_weight_ld", "vae2_conv2d_multi", "vae2_wgrad_flush")
+            "vae2_conv2d_bwd_weight_ld", "vae2_conv2d_multi", "vae2_wgrad_flush",
+            # BatchNorm fused into the consumer conv (ops.LazyBN: dconv3 / wgrad3 BNX = 1, 2)
+            "vae2_conv2d_fwd_bnin", "vae2_conv2d_bwd_weight_bnin", "vae2_conv2d_bwd_data_bnpart")
 HEAD_ABI = ("vae2_conv1x1_upsum_fwd", "vae2_head_out_fwd", "vae2_head_out_bwd_reduce",
             "vae2_head_out_bwd_apply", "vae2_upsample_bilinear_bwd_multi",
             "vae2_bn_reduce_finalize_shifted")
@@ -61,7 +63,7 @@ class Recorder:
         rc = fn(*args)
         n = self.lib.vae2_kernel_log_read(self.buf, len(self.buf))
         ks = self.buf.value.decode().split(";") if n > 0 else []
-        if desc and desc[0][0] == "wgrad":  # reduction deferred to vae2_wgrad_flush or not
+        if desc and desc[0][0] in ("wgrad", "wgrad_bnin"):  # reduction deferred to vae2_wgrad_flush or not
             desc = [d + (not any(k.startswith("wgrad_reduce_kernel") for k in ks),) for d in desc]
         self.calls.append((name, desc, ks))
         return rc
@@ -106,6 +108,19 @@ def describe(name, args):
             xp, xa, dyp, dya, dw, _ld, db, k, s, pad, acc = args[:11]
         return [("wgrad", _act(xa), _al(xp), _act(dya), _al(dyp), k, s, pad, int(acc),
                  db is not None and _al(db) is not None)]
+    if name == "vae2_conv2d_fwd_bnin":
+        xp, xa, _save, relu, wp, bias, yp, ya, k, s, pad, beta, stats, _ = args
+        return [("fwd_bnin", _act(xa), _al(xp), _act(ya), _al(yp), k, s, pad,
+                 float(beta) != 0.0, bias is not None and _al(bias) is not None,
+                 stats is not None and _al(stats) is not None, int(relu))]
+    if name == "vae2_conv2d_bwd_weight_bnin":
+        xp, xa, _save, relu, dyp, dya, dw, db, k, s, pad, acc = args[:12]
+        return [("wgrad_bnin", _act(xa), _al(xp), _act(dya), _al(dyp), k, s, pad, int(acc),
+                 db is not None and _al(db) is not None, int(relu))]
+    if name == "vae2_conv2d_bwd_data_bnpart":
+        dyp, dya, wp, dxp, dxa, k, s, pad, bxp, bxa, _save, relu, _part, _ = args
+        return [("dgrad_bnpart", _act(dya), _al(dyp), _act(dxa), _al(dxp), k, s, pad,
+                 _act(bxa), _al(bxp), int(relu))]
     if name == "vae2_conv2d_multi":
         n, arr, _ = args
         jobs = ctypes.cast(arr, ctypes.POINTER(_job_type()))
@@ -255,6 +270,133 @@ def _replay_wgrad(key, lib):
         assert rel(db.cpu(), rb) < 1e-5, (key, rel(db.cpu(), rb))
 
 
+def _bn_save(c, g, relu_frac=0.5):
+    """A BatchNorm layer's (mean, invstd, scale, shift) with some channels' shift making
+    the ReLU cut a good share of the pixels (random, not the reference init's ~identity)."""
+    mean = 0.3 * torch.randn(c, generator=g)
+    invstd = 0.5 + torch.rand(c, generator=g)
+    gamma = 1.0 + 0.5 * torch.randn(c, generator=g)
+    beta = relu_frac * torch.randn(c, generator=g)
+    scale = gamma * invstd
+    return torch.cat([mean, invstd, scale, beta - mean * scale]).contiguous()
+
+
+def _normalised(x, save, relu):
+    """The stored path's input: relu?(x * scale + shift) on CPU (NCHW)."""
+    c = x.shape[1]
+    z = x * save[2 * c:3 * c].view(1, c, 1, 1) + save[3 * c:].view(1, c, 1, 1)
+    return z.clamp_min(0.0) if relu else z
+
+
+def _replay_fwd_bnin(key, lib):
+    """conv(relu(bn(r))) with bn applied while staging r, vs normalise-then-conv on CPU."""
+    from vae2 import ops
+    _, xa, xal, ya, yal, k, s, pad, beta, has_bias, has_stats, relu = key
+    x, _ = _buffer(xa, xal)
+    y, _ = _buffer(ya, yal)
+    y0 = y.clone()
+    cout, cin = ya[3], xa[3]
+    g = torch.Generator().manual_seed(zlib.crc32(repr(key).encode()))
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(DEV)
+    b = (0.1 * torch.randn(cout, generator=g)).to(DEV) if has_bias else None
+    save = _bn_save(cin, g)
+    save_d = save.to(DEV)
+    xp, xact = ops.act_of(x)
+    yp, yact = ops.act_of(y)
+    stats, rows = None, 0
+    if has_stats:
+        rows = lib.vae2_conv2d_fwd_stats_rows(xp, ctypes.byref(xact), ctypes.byref(yact), k, s,
+                                              pad)
+        stats = torch.empty(2 * rows * cout, device=DEV)
+    ops.call("vae2_conv2d_fwd_bnin", xp, ctypes.byref(xact), ops.ptr(save_d), relu,
+             ops.ptr(ops.packed_weight(w, 0)), ops.ptr(b), yp, ctypes.byref(yact), k, s, pad,
+             1.0 if beta else 0.0, ops.ptr(stats), ops.stream_ptr())
+    torch.cuda.synchronize()
+    z = _normalised(_nchw(x), save, relu)
+    ref = F.conv2d(z, w.cpu(), b.cpu() if b is not None else None, s, pad)
+    if beta:
+        ref = ref + _nchw(y0)
+    got = _nchw(y)
+    assert rel(got, ref) < 2e-5, (key, rel(got, ref))
+    if has_stats:
+        st = stats.view(2, rows, cout).double().sum(1).cpu()
+        want = torch.stack([got.double().sum((0, 2, 3)), (got.double() ** 2).sum((0, 2, 3))])
+        assert rel(st, want) < 1e-5, (key, rel(st, want))
+
+
+def _replay_wgrad_bnin(key, lib):
+    """dW of conv(relu(bn(r))) with bn applied to the staged r, vs CPU fp32."""
+    from vae2 import ops
+    _, xa, xal, dya, dyal, k, s, pad, acc, has_bias, relu, deferred = key
+    x, _ = _buffer(xa, xal)
+    dy, _ = _buffer(dya, dyal)
+    cout, cin = dya[3], xa[3]
+    g = torch.Generator().manual_seed(zlib.crc32(repr(key).encode()))
+    save = _bn_save(cin, g)
+    save_d = save.to(DEV)
+    dw = torch.randn(cout, cin, k, k, device=DEV)
+    dw0 = dw.clone()
+    db = torch.randn(cout, device=DEV) if has_bias else None
+    xp, xact = ops.act_of(x)
+    dyp, dyact = ops.act_of(dy)
+    size = lib.vae2_conv2d_bwd_weight_ws_size(ctypes.byref(xact), ctypes.byref(dyact), k)
+    ws = torch.empty(max(size, 1), device=DEV)
+    lib.vae2_wgrad_defer(1 if deferred else 0)
+    try:
+        ops.call("vae2_conv2d_bwd_weight_bnin", xp, ctypes.byref(xact), ops.ptr(save_d),
+                 relu, dyp, ctypes.byref(dyact), ops.ptr(dw), ops.ptr(db), k, s, pad, acc,
+                 ops.ptr(ws), size, ops.stream_ptr())
+        if deferred:
+            ops.call("vae2_wgrad_flush", ops.stream_ptr())
+    finally:
+        lib.vae2_wgrad_defer(0)
+    torch.cuda.synchronize()
+    z = _normalised(_nchw(x), save, relu)
+    ref = conv2d_weight(z, (cout, cin, k, k), _nchw(dy), s, pad)
+    if acc:
+        ref = ref + dw0.cpu()
+    assert rel(dw.cpu(), ref) < 1e-4, (key, rel(dw.cpu(), ref))
+
+
+def _replay_dgrad_bnpart(key, lib):
+    """dX of the consumer conv plus the producer BatchNorm's backward partials
+    (sum g, sum g*xhat with g = dX masked by the ReLU recomputed from r) from its epilogue:
+    dX vs CPU fp32, the partials' sums vs fp64 of the same terms."""
+    from vae2 import ops
+    _, dya, dyal, dxa, dxal, k, s, pad, bxa, bxal, relu = key
+    dy, _ = _buffer(dya, dyal)
+    dx, _ = _buffer(dxa, dxal)
+    r, _ = _buffer(bxa, bxal)
+    cout, cin = dya[3], dxa[3]
+    g = torch.Generator().manual_seed(zlib.crc32(repr(key).encode()))
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cout * k * k) ** 0.5).to(DEV)
+    save = _bn_save(cin, g)
+    save_d = save.to(DEV)
+    dyp, dyact = ops.act_of(dy)
+    dxp, dxact = ops.act_of(dx)
+    rp, ract = ops.act_of(r)
+    rows = lib.vae2_conv2d_bwd_data_bnpart_rows(dyp, ctypes.byref(dyact), ctypes.byref(dxact), k,
+                                                s, pad)
+    assert rows > 0, key
+    part = torch.empty(2 * rows * cin, device=DEV)
+    ops.call("vae2_conv2d_bwd_data_bnpart", dyp, ctypes.byref(dyact),
+             ops.ptr(ops.packed_weight(w, 1)), dxp, ctypes.byref(dxact), k, s, pad, rp,
+             ctypes.byref(ract), ops.ptr(save_d), relu, ops.ptr(part), ops.stream_ptr())
+    torch.cuda.synchronize()
+    n, h, wd, _, _ = dxa
+    ref = conv2d_input((n, cin, h, wd), w.cpu(), _nchw(dy), s, pad)
+    assert rel(_nchw(dx), ref) < 2e-5, (key, rel(_nchw(dx), ref))
+    gd = _nchw(dx).double()  # the partials are of the kernel's own dX
+    rd = _nchw(r).double()
+    sd = save.double()
+    if relu:
+        gd = torch.where(_normalised(rd, sd, False) > 0, gd, torch.zeros_like(gd))
+    xh = (rd - sd[:cin].view(1, cin, 1, 1)) * sd[cin:2 * cin].view(1, cin, 1, 1)
+    exact = torch.stack([gd.sum((0, 2, 3)), (gd * xh).sum((0, 2, 3))])
+    got = part.view(2, rows, cin).double().sum(1).cpu()
+    assert rel(got, exact) < 1e-5, (key, rel(got, exact))
+
+
 def _kernels(calls, names, fams=None):
     out = set()
     for name, _, ks in calls:
@@ -275,16 +417,24 @@ def test_conv_instances_at_bench_geometry(bench_step):
                 if kk not in keys:
                     keys.append(kk)
     assert any(k[0] == "fwd" for k in keys) and any(k[0] == "wgrad" for k in keys)
+    # the LazyBN calls of the bench step are among the recorded ones (BNX = 1 / 2 kernels)
+    assert all(any(k[0] == kind for k in keys)
+               for kind in ("fwd_bnin", "wgrad_bnin", "dgrad_bnpart")), sorted({k[0] for k in keys})
     want = _kernels(bench_step, CONV_ABI)
+    replay = {"fwd": _replay_fwd, "dgrad": _replay_dgrad, "wgrad": _replay_wgrad,
+              "fwd_bnin": _replay_fwd_bnin, "wgrad_bnin": _replay_wgrad_bnin,
+              "dgrad_bnpart": _replay_dgrad_bnpart}
     with Recorder() as rec:
         for key in keys:
-            {"fwd": _replay_fwd, "dgrad": _replay_dgrad, "wgrad": _replay_wgrad}[key[0]](key, lib)
+            replay[key[0]](key, lib)
     got = _kernels(rec.calls, CONV_ABI)
     want = {k for k in want if _family(k) in ("conv_fwd", "conv_dgrad", "conv_wgrad",
                                              "conv_1x1")}
     missing = sorted(want - got)
     assert not missing, missing
-    print(f"{len(keys)} distinct conv calls, {len(want)} kernel instances replayed")
+    print(f"{len(keys)} distinct conv calls, {len(want)} kernel instances replayed:")
+    for k in sorted(want):
+        print("  ", k)
 
 
 def _ref_block_module(m, xs):

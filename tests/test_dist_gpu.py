@@ -127,3 +127,139 @@ def test_two_ranks_one_gpu_sync_bn_matches_reference():
         assert same, "batched SyncBN exchange differs from the per-layer exchange"
         assert n_batched < n_layer, (n_batched, n_layer)
     assert res[0][4] == res[1][4]  # identical averaged gradients on both ranks
+
+
+# ---------------------------------------------------------------------------------------
+# W18 at 64x128: the production-width HIP path (direct 3x3 kernels, LazyBN, the depth-level
+# SyncBN exchange grouping, per-branch heads) with 2 ranks x 1 clip against the oracle's
+# 1 rank x 2 clips (SyncBatchNorm + DDP's mean, tools/train.py:216-229).
+W18_HW = (64, 128)
+
+
+def _w18_inputs():
+    gen = torch.Generator().manual_seed(21)
+    xs = [torch.randn(2, 9, *W18_HW, generator=gen) for _ in range(3)]
+    eps = torch.randn(2, 10, 1, 1, generator=gen)
+    code = torch.randn(2, 10, 1, 1, generator=gen)
+    return xs, eps, code
+
+
+def _w18_work(rank, world, port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from helpers import build, make_cfg
+    from vae2 import dist as vdist
+    from vae2.model import FullModel_encdec
+    from vae2.optim import FusedAdam
+    dev = "cuda:0"
+    vdist.set_sync_bn(True)
+    calls = [0]
+    orig = vdist.all_reduce_
+
+    def counting(t_, group=None):
+        calls[0] += 1
+        return orig(t_, group=group)
+    vdist.all_reduce_ = counting
+    kw = dict(arch="w18", hw=W18_HW)
+    ed, ez = build(make_cfg(**kw))
+    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(dev)
+    fm.train()
+    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-4)
+    xs, eps, code = _w18_inputs()
+    sl = slice(rank, rank + 1)
+    fm.set_noise(eps[sl], code[sl])
+    opt.zero_grad()
+    losses, _, x2p, x3p = fm(*[x[sl].to(dev) for x in xs], 1.0)
+    losses[0].backward()
+    torch.cuda.synchronize()
+    exchanges = calls[0]
+    vdist.allreduce_grads(opt.flats)
+    torch.cuda.synchronize()
+    vdist.all_reduce_ = orig
+    loss = losses[0].detach().clone()
+    orig(loss)
+    gsum = float(torch.cat([f.grad for f in opt.flats]).double().sum())
+    out = [float(loss) / world, x2p.detach().cpu(), x3p.detach().cpu(), gsum, exchanges]
+    if rank == 0:  # the averaged gradients (identical on both ranks: gsum) per parameter
+        from test_model_gpu import named_params
+        out.append({n: p.main_grad.detach().cpu().clone() for n, p in
+                    named_params(("encz", fm.encz_model), ("ed", fm.encdec_model))})
+    q.put((rank, "ok", *out))
+    dist.destroy_process_group()
+
+
+def _w18_worker(rank, world, port, q):
+    try:
+        _w18_work(rank, world, port, q)
+    except BaseException:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_w18_sync_bn_matches_oracle():
+    """2 ranks x 1 clip (SyncBN exchanges per depth level over gloo, gradient mean) equal
+    the oracle's 1 rank x 2 clips: the mean loss within 1e-5, x2t_hat within 1e-4 and the
+    decoder frames within 1e-3, every averaged parameter gradient against
+    the fp64 oracle with the calibrated rule of test_model_gpu (fp32 oracle distance and
+    the fp64 oracle's own sensitivity to 1e-6 input noise), identical gradients on both
+    ranks."""
+    from oracle import ref_cpu
+    from test_model_gpu import check_grads_calibrated, oracle_elbo_grads
+    from helpers import build, make_cfg, max_rel
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_w18_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    import queue
+    import time
+    res, deadline = [], time.time() + 420
+    while len(res) < len(procs):
+        try:
+            res.append(q.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"2-rank W18 run failed: exit codes {[p.exitcode for p in procs]}")
+    for p in procs:
+        p.join(timeout=60)
+    errors = [r for r in res if r[1] == "error"]
+    assert not errors, errors[0][2]
+    res = sorted(res, key=lambda r: r[0])
+    kw = dict(arch="w18", hw=W18_HW)
+    xs, eps, code = _w18_inputs()
+    ed, ez = build(make_cfg(**kw))
+    with torch.no_grad():
+        terms, preds, _ = ref_cpu.elbo(ez, ed, *xs, eps, code)
+    ref_loss = float(terms["loss_all"])
+    loss = res[0][2]
+    assert abs(res[1][2] - loss) <= 1e-7 * abs(loss)  # the reduced loss on both ranks
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
+    x2 = torch.cat([res[0][3], res[1][3]])
+    x3 = torch.cat([res[0][4], res[1][4]])
+    assert max_rel(x2, preds[1]) < 1e-4, max_rel(x2, preds[1])
+    assert max_rel(x3, preds[2]) < 1e-3, max_rel(x3, preds[2])
+    assert res[0][5] == res[1][5]  # identical averaged gradients on both ranks
+    assert res[0][6] < 600, res[0][6]  # SyncBN exchanges per step, batched per depth level
+    grads = res[0][7]
+
+    class _P:
+        def __init__(self, g):
+            self.main_grad = g
+    params = [(n, _P(g)) for n, g in grads.items()]
+    g64 = oracle_elbo_grads(kw, None, torch.float64, xs=xs, noise_=(eps, code))
+    g32 = oracle_elbo_grads(kw, None, torch.float32, xs=xs, noise_=(eps, code))
+    g64p = oracle_elbo_grads(kw, None, torch.float64, xs=xs, noise_=(eps, code), perturb=1e-6)
+    med_hip, med_ref = check_grads_calibrated(params, g32, g64, g64p=g64p)
+    print(f"W18 2 ranks x 1 clip: loss {loss:.6f} (oracle {ref_loss:.6f}), x2t max-rel "
+          f"{max_rel(x2, preds[1]):.2e}, median grad distance to fp64 {med_hip:.3e} "
+          f"(fp32 oracle {med_ref:.3e}), {res[0][6]} SyncBN exchanges")

@@ -63,8 +63,16 @@ def _work(port, q):
         calls[0] += 1
         return orig(t_, group=group)
     vdist.all_reduce_ = counting
+    vdist.EARLY_CHECK = []
     fm, opt, loss, x2p, _ = _step(dev, g, FullModel_encdec, build, make_cfg, t, FusedAdam)
+    torch.cuda.synchronize()
     exchanges = calls[0]
+    # the early buckets read the decoders' tail when the x2t_hat hook fired (after the
+    # flush of the queued dW reductions and the side-stream join): nothing the rest of the
+    # backward ran may write it afterwards (at world 1 the all-reduce is an identity)
+    tail_final = (len(vdist.EARLY_CHECK) >= 1 and
+                  all(torch.equal(b[s:], snap) for b, s, snap in vdist.EARLY_CHECK))
+    vdist.EARLY_CHECK = None
     # the decoders' buckets were started from the x2t_hat hook during backward
     early = {k: (v[0], len(v[1])) for k, v in vdist._EARLY.items()}
     ed_flat = opt.flats[1]
@@ -81,7 +89,7 @@ def _work(port, q):
     early_ok = (early.get(id(ed_flat), (None, 0))[0] == vdist.tail_range(ed_flat) and
                 early[id(ed_flat)][1] >= 1)
     q.put(("ok", got[0], float(red), float(g["loss_loss_all"]), fwd_same, grad_rel, exchanges,
-           base_same, grad_same, early_ok))
+           base_same, grad_same, early_ok, tail_final))
     dist.destroy_process_group()
 
 
@@ -109,13 +117,14 @@ def test_rccl_world1_dist_path_equals_single_process_step():
     p.join(timeout=60)
     assert res[0] == "ok", res[1]
     (_, loss, reduced, ref, fwd_same, grad_rel, exchanges, base_same, grad_same,
-     early_ok) = res
+     early_ok, tail_final) = res
     print(f"grad rel {grad_rel:.3g}, single-process step deterministic: {base_same}, "
           f"distributed == single-process: {grad_same}, early decoder buckets: {early_ok}")
     assert abs(loss - ref) <= 1e-5 * abs(ref)
     assert reduced == loss
     assert exchanges > 50  # SyncBN statistics went through RCCL
     assert early_ok, "the decoders' gradient buckets did not start during backward"
+    assert tail_final, "the decoders' gradient tail changed after its buckets started"
     assert fwd_same, "the RCCL path changed the forward"
     if base_same:  # a deterministic step must stay bit-identical through the RCCL path
         assert grad_same, grad_rel

@@ -489,6 +489,7 @@ struct Gemm1 {
   float beta;
   float* stats;         // [2][gridDim.x][n] or null
   uint32_t a_bytes, w_bytes;
+  int vec;              // y 16-byte aligned with y_ps % 4 == 0 (else 4-byte stores)
 };
 
 template <int TM, int TN>
@@ -596,8 +597,8 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + j * 16 + qc;
-          yold[j] = (m < p.M && n + 3 < p.n) ? *reinterpret_cast<const f4*>(yrow + n)
-                                             : f4{0.f, 0.f, 0.f, 0.f};
+          yold[j] = (p.vec && m < p.M && n + 3 < p.n) ? *reinterpret_cast<const f4*>(yrow + n)
+                                                      : f4{0.f, 0.f, 0.f, 0.f};
         }
       }
 #pragma unroll
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] += n + q < p.n ? p.bias[n + q] : 0.f;
         }
-        if (n + 3 < p.n) {
+        if (p.vec && n + 3 < p.n) {
           if (p.beta != 0.f) v += p.beta * yold[j];
           *reinterpret_cast<f4*>(yrow + n) = v;
         } else {
@@ -2020,9 +2021,12 @@ static uint32_t act_bytes(const vae2_act* d) {
 int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
                  const G1Tile& t, hipStream_t s, const char* fn) {
-  // (16-byte stores of whole channel quads; statistics are of the fresh output only)
-  if (!vec_ok(y, (int)yd->ps) || (stats && beta != 0.f)) return -1;
+  // (16-byte stores of whole channel quads where y is aligned, 4-byte stores otherwise, so
+  // the statistics rows vae2_conv2d_fwd_stats_rows reports do not depend on y's alignment;
+  // statistics are of the fresh output only)
+  if (stats && beta != 0.f) return -1;
   Gemm1 p{};
+  p.vec = vec_ok(y, (int)yd->ps) ? 1 : 0;
   p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
   p.M = (int)act_pixels(yd);
   p.w = wp; p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;

@@ -32,6 +32,7 @@ _GRAD_GROUP = None
 _EARLY = {}       # id(flat) -> (flat, end offset already launched, [async works])
 FORCE = False     # the distributed code path at world size 1 (tests: bit-identity)
 OVERLAP = True    # early decoder buckets (A/B: off = everything after backward)
+EARLY_CHECK = None  # tests: a list the early hook appends (flat grad, start, tail snapshot) to
 
 
 def is_dist():
@@ -121,6 +122,8 @@ def early_reduce_hook(t, flat, start):
         ops.flush_wgrad()   # the decoders' queued weight-gradient reductions
         streams.join_all()  # the decoders' side-stream work
         buf = flat.grad
+        if EARLY_CHECK is not None:  # the tail as the buckets see it (no later write allowed)
+            EARLY_CHECK.append((buf, start, buf[start:].clone()))
         works = [dist.all_reduce(buf[off:off + BUCKET_ELEMS], group=grad_group(),
                                  async_op=True)
                  for off in range(start, buf.numel(), BUCKET_ELEMS)]

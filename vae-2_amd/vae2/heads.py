@@ -34,8 +34,8 @@ import torch
 
 from . import _lib, prof
 from ._lib import Act, call
-from .ops import (_WS_HOLD, _all_reduce_sums, _bn_group, _empty, _grad_sink, act_of, as_act,
-                  new_act, packed_weight_cols, ptr, stream_ptr, wgrad_batch)
+from .ops import (_WS_HOLD, _all_reduce_sums, _bn_group, _defer_off, _empty, _grad_sink, act_of,
+                  as_act, new_act, packed_weight_cols, ptr, stream_ptr, wgrad_batch)
 
 _PER_HEAD = 6  # conv weight, conv bias, BN weight, BN bias, out weight, out bias
 
@@ -238,10 +238,12 @@ class _Heads(torch.autograd.Function):
                             pj = xja.n * xja.h * xja.w
                             prof.note(2.0 * pj * xja.c * C, 4.0 * (pj * xja.c + pj * C + C * xja.c),
                                       prof.conv_label("head wgrad", xja.c, C, 1, 1, xja.h, xja.w))
-                        call("vae2_conv2d_bwd_weight_ld", xjp, ctypes.byref(xja), gp,
-                             ctypes.byref(ga), ctypes.c_void_p(wsink.data_ptr() + 4 * c0), C,
-                             None, 1, 1, 0, 1, ptr(ws2), wsz2, s)
-                        _WS_HOLD.append(ws2)
+                        with _defer_off(wret is not None):  # autograd takes wret on return
+                            call("vae2_conv2d_bwd_weight_ld", xjp, ctypes.byref(xja), gp,
+                                 ctypes.byref(ga), ctypes.c_void_p(wsink.data_ptr() + 4 * c0),
+                                 C, None, 1, 1, 0, 1, ptr(ws2), wsz2, s)
+                        if wret is None:
+                            _WS_HOLD.append(ws2)
                     if ctx.needs_input_grad[2 + j]:
                         first = dxs[j] is None
                         if first:

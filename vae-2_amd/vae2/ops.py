@@ -400,7 +400,7 @@ def _conv_fwd_queued(group, x, weight, bias, spec, stats):
 
 _WGRAD_BATCH = [0]  # open wgrad_batch contexts
 _WS_HOLD = []       # workspaces of queued weight-gradient reductions
-_WGRAD_CB = [False]  # an end-of-backward flush is queued with the autograd engine
+_WGRAD_CB = [False, -1]  # end-of-backward flush queued with the engine, by graph task id
 
 
 def flush_wgrad():
@@ -424,14 +424,28 @@ def _end_of_backward():
     flush_wgrad()
 
 
+def _graph_task():
+    """Id of the autograd graph task running on this thread (-1 outside a backward)."""
+    try:
+        return torch._C._current_graph_task_id()
+    except (AttributeError, RuntimeError):
+        return -1
+
+
 class wgrad_batch:
     """Context: the weight-gradient slab reductions of the convs in it are queued
     (vae2_wgrad_defer) and launched together, up to 32 per launch, once at the end of
     the backward pass (an autograd engine final callback; the early gradient buckets of
     vae2.dist flush first), or at the context's exit outside a backward.  Their
-    workspaces are held until then."""
+    workspaces are held until then.  Only reductions into flat-buffer ``main_grad``
+    views are deferred: a dW target handed to autograd is reduced at once
+    (_defer_off), since autograd reads it as soon as the backward function returns."""
 
     def __enter__(self):
+        if _WGRAD_BATCH[0] == 0 and _WGRAD_CB[0] and _WGRAD_CB[1] != _graph_task():
+            # the backward that queued the end-of-backward flush raised before the engine
+            # ran its final callbacks (it drops them): flush the stale queue now
+            _end_of_backward()
         _lib.load().vae2_wgrad_defer(1)
         _WGRAD_BATCH[0] += 1
         return self
@@ -443,9 +457,29 @@ class wgrad_batch:
             if not _WGRAD_CB[0]:
                 try:
                     torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-                    _WGRAD_CB[0] = True
+                    _WGRAD_CB[0], _WGRAD_CB[1] = True, _graph_task()
                 except RuntimeError:  # not inside a backward pass: flush now
                     flush_wgrad()
+        return False
+
+
+class _defer_off:
+    """The weight-gradient reductions issued inside run now, deferral or not (their dW
+    target is not a main_grad view: autograd consumes it when the backward returns)."""
+
+    __slots__ = ("on", "prev")
+
+    def __init__(self, on=True):
+        self.on = on
+
+    def __enter__(self):
+        if self.on:
+            self.prev = _lib.load().vae2_wgrad_defer(0)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _lib.load().vae2_wgrad_defer(self.prev)
         return False
 
 
@@ -467,19 +501,17 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         if prof.active():
             _conv_work("wgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         lz = spec.bn_in
-        if lz is not None:
-            call("vae2_conv2d_bwd_weight_bnin", xp, ctypes.byref(xa), ptr(lz.save),
-                 int(lz.relu), dyp, ctypes.byref(dya), ptr(wsink), ptr(bsink), spec.k,
-                 spec.stride, spec.pad, 1, ptr(ws), size, s)
-        else:
-            call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya),
-                 ptr(wsink), ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
-        if _WGRAD_BATCH[0]:
-            # the deferred reduction writes wsink at the flush: a temporary dW target
-            # must outlive it like the workspace
-            _WS_HOLD.append(ws)
-            if tmp_w:
-                _WS_HOLD.append(wsink)
+        now = wret is not None or tmp_w  # not a main_grad view: reduce before returning
+        with _defer_off(now and _WGRAD_BATCH[0] > 0):
+            if lz is not None:
+                call("vae2_conv2d_bwd_weight_bnin", xp, ctypes.byref(xa), ptr(lz.save),
+                     int(lz.relu), dyp, ctypes.byref(dya), ptr(wsink), ptr(bsink), spec.k,
+                     spec.stride, spec.pad, 1, ptr(ws), size, s)
+            else:
+                call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya),
+                     ptr(wsink), ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
+        if _WGRAD_BATCH[0] and not now:
+            _WS_HOLD.append(ws)  # the deferred reduction reads it at the flush
     dx = None
     if need_dx:
         link = spec.x_link
