@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 9
+#define VAE2_ABI_VERSION 10
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -304,6 +304,20 @@ typedef struct vae2_bn_layer {
   int relu;
   int dres_acc;                   /* backward apply: 1 = dres += masked dy (the residual  */
                                   /* gradient summed onto another consumer's, in-kernel) */
+  /* ABI 10: the residual through its own BatchNorm (no ReLU) whose normalised output is
+   * never stored -- the Bottleneck's downsample shortcut (enc_hrnet.py:94-101, replaces
+   * a separate apply pass, backward reduce pass and backward apply pass of that BN).
+   * rx = NULL: none.  Forward (a must be NULL): y = relu?(fma(x, scale, shift) +
+   * fma(rx, rsave.scale, rsave.shift)).  Backward (dres must be NULL): the residual BN's
+   * partials (sum g, sum g*xhat_r) into rpartials (reduce) and its input gradient
+   * rgamma*rinvstd*(g - rsums_g/count - xhat_r*rsums_gx/count) into rdx (apply), g =
+   * this layer's masked dy.  Same pixels and channels as x.                            */
+  const float* rx; vae2_act rxd;
+  const float* rsave;             /* [4][c] of the residual BN                          */
+  const float* rgamma;            /* backward apply (NULL: 1)                            */
+  float* rpartials;               /* backward reduce: [2][vae2_bn_partial_rows(xd)][c]  */
+  const double* rsums;            /* backward apply: the residual BN's [2][c] sums       */
+  float* rdx; vae2_act rdxd;      /* backward apply: the residual BN's input gradient   */
 } vae2_bn_layer;
 /* y = relu?(fma(x, scale, shift) + a) per layer (vae2_bn_apply).                 */
 int vae2_bn_multi_apply(int n, const vae2_bn_layer* layers, void* stream);

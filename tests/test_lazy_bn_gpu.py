@@ -156,3 +156,47 @@ def test_bnpart_partials_equal_bwd_reduce():
     exact = torch.stack([g.sum(0), (g * (xx - mean.double()) * invstd.double()).sum(0)])
     assert rel(got, exact) < 1e-5
     assert rel(ref, exact) < 1e-5
+
+
+def _bottleneck_run(flags, monkeypatch, shape=(2, 64, 128), seed=3):
+    """Bottleneck(64 -> 4 x 64, downsample) = layer1's first block, training BN."""
+    from vae2 import hrnet, ops
+    lazy, resbn = flags
+    monkeypatch.setattr(ops, "LAZY_BN", lazy)
+    monkeypatch.setattr(ops, "RES_BN", resbn)
+    torch.manual_seed(seed)
+    blk = hrnet.make_layer(hrnet.Bottleneck, 64, 64, 2).to(DEV)
+    for m in blk.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.normal_(m.weight, 1.0, 0.3)
+            nn.init.normal_(m.bias, 0.0, 0.3)
+        elif isinstance(m, nn.Conv2d):
+            nn.init.normal_(m.weight, 0.0, (2.0 / m.weight[0].numel()) ** 0.5)
+    n, h, w = shape
+    torch.manual_seed(seed + 1)
+    x = ops.new_act((n, h, w, 64), torch.empty(1, device=DEV))
+    with torch.no_grad():
+        x.normal_()
+    x.requires_grad_(True)
+    y = hrnet.run_seq(blk, x)
+    torch.manual_seed(seed + 2)
+    torch.autograd.backward([y], [torch.randn_like(y)])
+    torch.cuda.synchronize()
+    return blk, x, y
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 128), (3, 40, 72)])
+def test_resbn_shortcut_equals_stored(shape, monkeypatch):
+    """ops.ResBN (the Bottleneck's downsample BN added inside bn3's apply, its partials and
+    input gradient from bn3's backward kernels) and the Bottleneck's LazyBN bn1 against the
+    stored path: forward bit-identical, gradients and running statistics within fp32
+    summation-order noise."""
+    ba, xa, ya = _bottleneck_run((True, True), monkeypatch, shape)
+    bb, xb, yb = _bottleneck_run((False, False), monkeypatch, shape)
+    assert torch.equal(ya, yb)
+    assert rel_nz(xa.grad, xb.grad) < 1e-5
+    for (na, pa), (_, pb) in zip(ba.named_parameters(), bb.named_parameters()):
+        assert rel_nz(pa.grad, pb.grad) < 1e-5, na
+    for (na, ra), (_, rb_) in zip(ba.named_buffers(), bb.named_buffers()):
+        if "running" in na:
+            assert torch.equal(ra, rb_), na

@@ -570,6 +570,16 @@ struct BnLayer {
   int64_t P, ppb;
   int C, x_ps, a_ps, o_ps, dy_ps, dres_ps, relu, rows, blk0;
   int dres_acc;         // backward apply: dres += g instead of dres = g
+  // residual through its own BatchNorm (no ReLU) whose output is never stored (the
+  // Bottleneck's downsample shortcut): forward adds fma(rx, rscale, rshift); backward
+  // writes that BN's partials (rpart) / input gradient (rdx) beside this layer's
+  const float* rx;
+  const float* rsave;
+  const float* rgamma;
+  float* rpart;
+  const double* rsums;
+  float* rdx;
+  int rx_ps, rdx_ps;
 };
 
 struct BnMulti {
@@ -589,6 +599,8 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
   if (tid >= L.rows * c4) return;
   const int r = tid / c4, c = 4 * (tid - r * c4);
   const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
+  f4 rsc = {0.f, 0.f, 0.f, 0.f}, rsh = rsc;
+  if (L.rx) { rsc = chan4(L.rsave + 2 * C, c, C); rsh = chan4(L.rsave + 3 * C, c, C); }
   const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
   f4 v[kApplyU], rv[kApplyU];
 #pragma unroll
@@ -597,6 +609,7 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
     if (p < L.P) {
       v[u] = ld4(L.x + p * L.x_ps + c);
       if (L.a) rv[u] = ld4(L.a + p * L.a_ps + c);
+      else if (L.rx) rv[u] = ld4(L.rx + p * L.rx_ps + c);
     }
   }
 #pragma unroll
@@ -608,6 +621,8 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
     for (int k = 0; k < 4; ++k) {
       float t = __builtin_fmaf(v[u][k], sc[k], sh[k]);
       if (L.a) t += rv[u][k];
+      // the residual BN's output, rounded as if stored, then added
+      else if (L.rx) t += __builtin_fmaf(rv[u][k], rsc[k], rsh[k]);
       o[k] = (L.relu && t < 0.f) ? 0.f : t;  // NaN propagates (torch.relu)
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
@@ -627,16 +642,19 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
   const int64_t p0 = blk * L.ppb;
   int64_t p1 = p0 + L.ppb;
   if (p1 > L.P) p1 = L.P;
-  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s0;
   const int r = tid / c4, c = 4 * (tid - r * c4);
   const float* y = L.relu ? L.a : nullptr;
+  const bool rb = L.rx != nullptr;  // + the residual BN's sum g * xhat_r (same g)
   if (tid < L.rows * c4) {
     const f4 mean = chan4(L.save, c, C), invstd = chan4(L.save + C, c, C);
     const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
+    f4 rmean = s0, rinv = s0;
+    if (rb) { rmean = chan4(L.rsave, c, C); rinv = chan4(L.rsave + C, c, C); }
     // kApplyU pixels' loads in flight per thread, then their math in pixel order (the
     // same accumulation order as one pixel at a time)
     for (int64_t pb = p0 + r; pb < p1; pb += (int64_t)kApplyU * L.rows) {
-      f4 xv[kApplyU], gv[kApplyU], yv[kApplyU];
+      f4 xv[kApplyU], gv[kApplyU], yv[kApplyU], rv[kApplyU];
 #pragma unroll
       for (int u = 0; u < kApplyU; ++u) {
         const int64_t p = pb + u * L.rows;
@@ -644,6 +662,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
           xv[u] = ld4(L.x + p * L.x_ps + c);
           gv[u] = ld4(L.dy + p * L.dy_ps + c);
           if (y) yv[u] = ld4(y + p * L.a_ps + c);
+          if (rb) rv[u] = ld4(L.rx + p * L.rx_ps + c);
         }
       }
 #pragma unroll
@@ -657,6 +676,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
             ga[k] = 0.f;
           s0[k] += ga[k];
           s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+          if (rb) s2[k] += ga[k] * (rv[u][k] - rmean[k]) * rinv[k];
         }
       }
     }
@@ -675,6 +695,19 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
     }
     L.part[(int64_t)blk * C + ch] = a;
     L.part[((int64_t)nblk + blk) * C + ch] = b;
+    if (rb) L.rpart[(int64_t)blk * C + ch] = a;  // the residual BN's sum g: the same sum
+  }
+  if (!rb) return;
+  __syncthreads();
+  if (tid < L.rows * c4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red1[r * 4 * c4 + c + k] = s2[k];
+  }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    float b = 0.f;
+    for (int i = 0; i < L.rows; ++i) b += red1[i * 4 * c4 + ch];
+    L.rpart[((int64_t)nblk + blk) * C + ch] = b;
   }
 }
 
@@ -694,7 +727,9 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   const double count = L.countp ? *L.countp : L.count;
   const float inv_n = (float)(1.0 / count);
   const float* y = L.relu ? L.a : nullptr;
+  const bool rb = L.rx != nullptr;
   f4 mean, invstd, sc, sh, mg, mgx, k4;
+  f4 rmean = {0.f, 0.f, 0.f, 0.f}, rinv = rmean, rmg = rmean, rmgx = rmean, rk4 = rmean;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int ch = c + k < C ? c + k : C - 1;
@@ -705,9 +740,16 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
     mg[k] = (float)L.sums[ch] * inv_n;
     mgx[k] = (float)L.sums[C + ch] * inv_n;
     k4[k] = (L.gamma ? L.gamma[ch] : 1.f) * invstd[k];
+    if (rb) {
+      rmean[k] = L.rsave[ch];
+      rinv[k] = L.rsave[C + ch];
+      rmg[k] = (float)L.rsums[ch] * inv_n;
+      rmgx[k] = (float)L.rsums[C + ch] * inv_n;
+      rk4[k] = (L.rgamma ? L.rgamma[ch] : 1.f) * rinv[k];
+    }
   }
   const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
-  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU];
+  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU], rxv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
     const int64_t p = pb + u * L.rows;
@@ -715,6 +757,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
       gv[u] = ld4(L.dy + p * L.dy_ps + c);
       xv[u] = ld4(L.x + p * L.x_ps + c);
       if (y) yv[u] = ld4(y + p * L.a_ps + c);
+      if (rb) rxv[u] = ld4(L.rx + p * L.rx_ps + c);
     }
   }
 #pragma unroll
@@ -733,6 +776,15 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
       st4(dr, L.dres_acc ? g + ld4(dr) : g, c, C);
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
+    if (rb) {  // the residual BN's input gradient from the same g (bn_bwd_apply's formula)
+      f4 ro;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float xh = (rxv[u][k] - rmean[k]) * rinv[k];
+        ro[k] = rk4[k] * (g[k] - rmg[k] - xh * rmgx[k]);
+      }
+      st4(L.rdx + p * L.rdx_ps + c, ro, c, C);
+    }
   }
 }
 
@@ -1075,6 +1127,15 @@ static bool bn_layer_quad_ok(const vae2_bn_layer& l, bool bwd) {
       return false;
     if (l.dres && (!v4_ok(l.dres, l.dresd.ps) || l.dresd.c != x.c)) return false;
   }
+  if (l.rx) {  // the residual BN's input (and its gradient): same pixels and channels
+    const vae2_act& r = l.rxd;
+    if (!l.rsave || !v4_ok(l.rx, r.ps) || r.n != x.n || r.h != x.h || r.w != x.w || r.c != x.c)
+      return false;
+    if (!bwd && l.a) return false;  // one residual: stored (a) or through its BN (rx)
+    if (bwd && (l.dres || !l.rdx || !v4_ok(l.rdx, l.rdxd.ps) || l.rdxd.c != x.c ||
+                l.rdxd.n != x.n || l.rdxd.h != x.h || l.rdxd.w != x.w))
+      return false;
+  }
   return act_pixels(&x) * x.c < (int64_t(1) << 31);
 }
 
@@ -1093,6 +1154,8 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
                    "matching shapes, C <= 1024");
       VAE2_REQUIRE(kind == 0 || (kind == 1 ? l.partials != nullptr : l.sums != nullptr), fn,
                    "missing partials / sums");
+      VAE2_REQUIRE(!l.rx || kind == 0 || (kind == 1 ? l.rpartials != nullptr : l.rsums != nullptr),
+                   fn, "missing the residual BatchNorm's partials / sums");
       VAE2_REQUIRE(kind != 2 || l.countp || l.count > 0, fn, "bad count");
       BnLayer& L = m.L[j];
       L.x = l.x; L.a = l.a; L.o = l.o; L.dy = l.dy; L.dres = l.dres; L.part = l.partials;
@@ -1104,6 +1167,9 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       L.dy_ps = (int)l.dyd.ps; L.dres_ps = (int)l.dresd.ps;
       L.dres_acc = l.dres_acc;
       L.relu = l.relu;
+      L.rx = l.rx; L.rsave = l.rsave; L.rgamma = l.rgamma; L.rpart = l.rpartials;
+      L.rsums = l.rsums; L.rdx = l.rdx;
+      L.rx_ps = (int)l.rxd.ps; L.rdx_ps = (int)l.rdxd.ps;
       L.rows = quad_rows(l.xd.c);
       L.blk0 = blocks;
       if (kind == 1) {

@@ -33,7 +33,9 @@ class BnLayer(ctypes.Structure):
     _fields_ = [("x", c_vp), ("xd", Act), ("a", c_vp), ("ad", Act), ("o", c_vp), ("od", Act),
                 ("dy", c_vp), ("dyd", Act), ("dres", c_vp), ("dresd", Act),
                 ("save", c_vp), ("gamma", c_vp), ("partials", c_vp), ("sums", c_vp),
-                ("countp", c_vp), ("count", c_f64), ("relu", c_int), ("dres_acc", c_int)]
+                ("countp", c_vp), ("count", c_f64), ("relu", c_int), ("dres_acc", c_int),
+                ("rx", c_vp), ("rxd", Act), ("rsave", c_vp), ("rgamma", c_vp),
+                ("rpartials", c_vp), ("rsums", c_vp), ("rdx", c_vp), ("rdxd", Act)]
 
 
 class BnFin(ctypes.Structure):
@@ -167,7 +169,7 @@ _SIGS = {
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lib = None
 
 

@@ -87,15 +87,36 @@ class Bottleneck(nn.Module):
 
     def run(self, x):
         link = ops.GradLink(2)  # x feeds conv1 and the shortcut (see BasicBlock.run)
-        out = ops.conv_bn(x, self.conv1, self.bn1, relu=True, x_link=link)
-        out = ops.conv_bn(out, self.conv2, self.bn2, relu=True)
+        # bn1's normalised output feeds only conv2 (3x3): normalised in conv2's staging
+        # where the direct 3x3 kernels run (ops.LazyBN, as in run_blocks_lockstep)
+        out = _lazy_pair(x, self.conv1, self.bn1, self.conv2, self.bn2, x_link=link)
         if self.downsample is None:
             return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=x, res_link=link)
+        if len(self.downsample) == 2:  # conv + BN: its output is only bn3's residual (ops.ResBN)
+            return ops.conv_bn_multi([out, x], [self.conv3, self.downsample[0]],
+                                     [self.bn3, self.downsample[1]], [True, False],
+                                     x_links=[None, link], res_bns=[1, None])[0]
         sc = _run_convbn_seq(self.downsample, x, link)
         return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=sc)
 
 
 BLOCKS = {"BASIC": BasicBlock, "BOTTLENECK": Bottleneck}
+
+
+def _lazy_pair(x, conv_a, bn_a, conv_b, bn_b, x_link=None):
+    """relu(bn_b(conv_b(relu(bn_a(conv_a(x)))))) where bn_a's output feeds only conv_b: with
+    the direct 3x3 kernels for conv_b it is never stored (ops.LazyBN) -- the Bottleneck's
+    bn1 -> conv2 (enc_hrnet.py:84-90) and the stem's bn1 -> conv2 (:788-793)."""
+    n, h, w, _ = x.shape
+    spec = ops.ConvSpec(conv_a)
+    oh, ow = spec.out_hw(h, w)
+    lz = ops.LazyBN() if ops.lazy_bn_ok((n, oh, ow, conv_a.out_channels), conv_b) else None
+    if lz is None:
+        out = ops.conv_bn(x, conv_a, bn_a, relu=True, x_link=x_link)
+        return ops.conv_bn(out, conv_b, bn_b, relu=True)
+    lazy = [lz]
+    out = ops.conv_bn_multi([x], [conv_a], [bn_a], True, x_links=[x_link], bn_outs=lazy)
+    return ops.conv_bn_multi(out, [conv_b], [bn_b], True, bn_ins=lazy)[0]
 
 
 def _run_convbn_seq(seq, x, x_link=None):
@@ -390,8 +411,7 @@ class HighResolutionNet(nn.Module):
     # ---- execution ----
     def _stem(self, prefix, x):
         g = lambda n: getattr(self, prefix + n)  # noqa: E731
-        x = ops.conv_bn(x, g("conv1"), g("bn1"), relu=True)
-        x = ops.conv_bn(x, g("conv2"), g("bn2"), relu=True)
+        x = _lazy_pair(x, g("conv1"), g("bn1"), g("conv2"), g("bn2"))
         return run_seq(g("layer1"), x)
 
     def _trunk_to_stage4_inputs(self, prefix, x):

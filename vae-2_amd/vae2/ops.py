@@ -155,6 +155,20 @@ class LazyBN:
 LAZY_BN = True  # False: every BatchNorm output is stored (A/B and parity tests)
 
 
+class ResBN:
+    """Marks a layer of a _ConvBNMulti level whose BatchNorm output (no ReLU) is only the
+    residual of another layer of the same level (the Bottleneck's downsample shortcut,
+    enc_hrnet.py:94-101): that layer's apply adds it as fma(r, scale, shift) and its
+    backward kernels produce this BN's partials and input gradient from the same masked
+    gradient (vae2_bn_layer.rx ...), so the shortcut's BN output is never stored and its
+    three BN passes do not run."""
+
+    __slots__ = ()
+
+
+RES_BN = True  # False: the shortcut BN output is stored (A/B and parity tests)
+
+
 def lazy_bn_ok(shape, conv):
     """Can `conv` (3x3 stride 1) consume a LazyBN output of NHWC `shape` (N,H,W,C)?
     (the direct 3x3 forward and weight-gradient kernels must run for it)"""
@@ -176,7 +190,7 @@ class ConvSpec:
     """Static description of a conv(+BN) call: geometry and module handles."""
 
     __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training", "x_link",
-                 "res_link", "bn_in", "bn_out")
+                 "res_link", "bn_in", "bn_out", "res_bn")
 
     def __init__(self, conv, bn=None, relu=False):
         kh, kw = conv.kernel_size
@@ -189,6 +203,7 @@ class ConvSpec:
         self.bn = bn
         self.x_link = self.res_link = None
         self.bn_in = self.bn_out = None  # LazyBN: BatchNorm fused into the consumer conv
+        self.res_bn = None  # index (in its level) of the layer whose BN output is the residual
         if bn is not None:
             if bn.momentum is None:
                 raise ValueError("cumulative-average BatchNorm (momentum=None) is not supported")
@@ -760,6 +775,9 @@ class _ConvBNMulti(torch.autograd.Function):
         ys, lay = [], []
         for i, (r, save, spec) in enumerate(zip(rs, saves, specs)):
             lz = spec.bn_out
+            if isinstance(lz, ResBN):  # added by its consumer's apply: r stands in for y
+                ys.append(r)
+                continue
             if lz is not None:  # normalised by the consumer conv: r stands in for y
                 lz.save, lz.relu, lz.part, lz.rows = save, spec.relu, None, 0
                 ys.append(r)
@@ -767,11 +785,17 @@ class _ConvBNMulti(torch.autograd.Function):
             y = new_act(tuple(r.shape), r)
             ys.append(y)
             res = L[i][5]
-            lay.append(_bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
-                                 spec.relu))
+            layer = _bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
+                              spec.relu)
+            if spec.res_bn is not None:
+                j = spec.res_bn
+                layer.rx, layer.rxd = rs[j].data_ptr(), act_of(rs[j])[1]
+                layer.rsave = saves[j].data_ptr()
+            lay.append(layer)
         if lay:
             if prof.active():
-                prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None else 2)
+                prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None or
+                                                    specs[i].res_bn is not None else 2)
                                  for i, r in enumerate(rs) if specs[i].bn_out is None))
             call("vae2_bn_multi_apply", len(lay), (_lib.BnLayer * len(lay))(*lay), s)
         ctx.specs = specs
@@ -801,8 +825,33 @@ class _ConvBNMulti(torch.autograd.Function):
         keep, drs, dress, red = [], [], [], []
         off = 0
         lib = _lib.load()
+        # a shortcut BN (ResBN) gets its partials / input gradient from its consumer's
+        # kernels: its buffers first, so the consumer's layer can point at them
+        resbuf, o_ = {}, 0
+        for i in range(n):
+            if isinstance(specs[i].bn_out, ResBN):
+                _, ra = act_of(rs[i])
+                rows = lib.vae2_bn_partial_rows(ctypes.byref(ra))
+                resbuf[i] = (_empty((2 * rows * cs[i],), rs[i]), rows,
+                             new_act(tuple(rs[i].shape), rs[i]), buf.data_ptr() + 8 * o_)
+            o_ += 2 * cs[i]
+        act = []  # layers with BN passes of their own (not ResBN)
         for i in range(n):
             r, y, save, spec = rs[i], ys[i], saves[i], specs[i]
+            if i in resbuf:
+                part, rows, dr, sums_p = resbuf[i]
+                gamma, beta = ctx.params[i][2], ctx.params[i][3]
+                gsink, gret = _grad_sink(gamma, need[1 + 6 * i + 3])
+                bsink, bret = _grad_sink(beta, need[1 + 6 * i + 4])
+                fins[i] = _lib.BnFin(part.data_ptr(), rows, cs[i], sums_p, None, ctx.counts[i],
+                                     None, None, None, None, None, 0.0, 0.0, None, _p(gsink),
+                                     _p(bsink))
+                keep.append((part,))
+                drs.append(dr)
+                dress.append((None, gret, bret))
+                off += 2 * cs[i]
+                continue
+            act.append(i)
             dy = dys[i]
             dy = as_act(dy) if dy is not None else torch.zeros_like(y)
             if not _bn_quad_ok(dy):  # e.g. a channel slice of a concatenation's gradient
@@ -831,8 +880,17 @@ class _ConvBNMulti(torch.autograd.Function):
             bsink, bret = _grad_sink(beta, need[1 + 6 * i + 4])
             sums_p = buf.data_ptr() + 8 * off
             countp = buf.data_ptr() + 8 * (tot + i) if group is not None else None
-            lay[i] = _bn_layer(r, y if ctx.has_res[i] else None, dr, dy, dres, save, gamma,
-                               part, sums_p, countp, ctx.counts[i], spec.relu, acc)
+            lay[i] = _bn_layer(r, y if ctx.has_res[i] or spec.res_bn is not None else None, dr,
+                               dy, dres, save, gamma, part, sums_p, countp, ctx.counts[i],
+                               spec.relu, acc)
+            if spec.res_bn is not None:  # the shortcut BN's passes ride on this layer's
+                j = spec.res_bn
+                rpart, _, rdr, rsums_p = resbuf[j]
+                lay[i].rx, lay[i].rxd = rs[j].data_ptr(), act_of(rs[j])[1]
+                lay[i].rsave = saves[j].data_ptr()
+                lay[i].rgamma = _p(ctx.params[j][2])
+                lay[i].rpartials, lay[i].rsums = rpart.data_ptr(), rsums_p
+                lay[i].rdx, lay[i].rdxd = rdr.data_ptr(), act_of(rdr)[1]
             fins[i] = _lib.BnFin(part.data_ptr(), rows, cs[i], sums_p, None, ctx.counts[i],
                                  None, None, None, None, None, 0.0, 0.0, None, _p(gsink),
                                  _p(bsink))
@@ -842,7 +900,9 @@ class _ConvBNMulti(torch.autograd.Function):
             off += 2 * cs[i]
         if red:
             if prof.active():
-                prof.note(0, sum(4.0 * rs[i].numel() * (3 if ctx.has_res[i] else 2) for i in red))
+                prof.note(0, sum(4.0 * rs[i].numel() * (2 + (1 if ctx.has_res[i] else 0) +
+                                                        (2 if specs[i].res_bn is not None else 0))
+                                 for i in red))
             call("vae2_bn_multi_bwd_reduce", len(red), (_lib.BnLayer * len(red))(*[lay[i] for i in red]),
                  s)
         call("vae2_bn_multi_reduce", n, fins, 1, s)  # local sums + dgamma / dbeta
@@ -850,9 +910,12 @@ class _ConvBNMulti(torch.autograd.Function):
             from . import dist as vdist
             vdist.all_reduce_(buf, group=group)
         if prof.active():
-            prof.note(0, sum(4.0 * r.numel() * (3 + (1 if h_ else 0) + (1 if d[0] is not None else 0))
-                             for r, h_, d in zip(rs, ctx.has_res, dress)))
-        call("vae2_bn_multi_bwd_apply", n, lay, s)
+            prof.note(0, sum(4.0 * rs[i].numel() * (3 + (1 if ctx.has_res[i] else 0) +
+                                                    (1 if dress[i][0] is not None else 0) +
+                                                    (3 if specs[i].res_bn is not None else 0))
+                             for i in act))
+        call("vae2_bn_multi_bwd_apply", len(act), (_lib.BnLayer * len(act))(*[lay[i] for i in act]),
+             s)
         grads = [None]
         cg = ConvGroup()  # the level's data gradients: direct-3x3 layers share launches
         with wgrad_batch():  # the level's weight-gradient reductions in one launch
@@ -902,7 +965,7 @@ BN_BATCH = True  # False: conv_bn_multi runs its layers one by one (A/B and pari
 
 
 def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=None,
-                  bn_outs=None, bn_ins=None):
+                  bn_outs=None, bn_ins=None, res_bns=None):
     """[conv_bn(xs[i], convs[i], bns[i], relu, residuals[i], ...)] for independent layers,
     their BatchNorm steps batched into shared launches (training mode; with SyncBN one
     statistics exchange per direction for all of them).
@@ -910,7 +973,12 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
     bn_outs[i] (a LazyBN, or None): layer i's BatchNorm output is consumed only by a conv
     that takes it lazily -- the returned tensor is then the pre-BN conv output, to be
     passed on with bn_ins[i] = that LazyBN to the consumer's conv_bn_multi call.  Where
-    the batched path does not run, the entry is set to None (the output is stored)."""
+    the batched path does not run, the entry is set to None (the output is stored).
+
+    res_bns[i] (an index j, or None): layer i's residual is layer j's BatchNorm output
+    (layer j: no ReLU, no residual of its own, same output shape), added in layer i's
+    apply and never stored (ResBN); layer j's entry of the returned list is then its
+    pre-BN conv output, for no other use."""
     n = len(xs)
     residuals = residuals if residuals is not None else [None] * n
     x_links = x_links if x_links is not None else [None] * n
@@ -925,14 +993,31 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
         if bn_ins is not None:
             spec.bn_in = bn_ins[i]
         specs.append(spec)
-    if (not BN_BATCH or not all(sp.training for sp in specs) or
+    if res_bns is not None:
+        for i, j in enumerate(res_bns):
+            if j is None:
+                continue
+            if (residuals[i] is not None or residuals[j] is not None or relus[j] or
+                    res_bns[j] is not None or (bn_outs is not None and bn_outs[i] is not None)):
+                raise ValueError("res_bns: the shortcut layer must be a plain conv + BN")
+            specs[i].res_bn = j
+            specs[j].bn_out = ResBN()
+    if (not BN_BATCH or not RES_BN and res_bns is not None and any(j is not None for j in res_bns)
+            or not all(sp.training for sp in specs) or
             not all(r is None or _bn_quad_ok(r) for r in residuals)):
         if any(sp.bn_in is not None for sp in specs):
             raise RuntimeError("a LazyBN input needs the batched training path")
         if bn_outs is not None:
             bn_outs[:] = [None] * n
-        return [conv_bn(xs[i], convs[i], bns[i], relus[i], residuals[i], x_links[i],
-                        res_links[i]) for i in range(n)]
+        outs = [None] * n
+        order = [j for j in range(n) if res_bns is not None and j in res_bns]
+        order += [i for i in range(n) if i not in order]
+        for i in order:  # shortcut layers first: stored, then used as the residual
+            res = residuals[i]
+            if res_bns is not None and res_bns[i] is not None:
+                res = outs[res_bns[i]]
+            outs[i] = conv_bn(xs[i], convs[i], bns[i], relus[i], res, x_links[i], res_links[i])
+        return outs
     flat = []
     for i in range(n):
         flat += [xs[i], convs[i].weight, convs[i].bias, bns[i].weight, bns[i].bias, residuals[i]]
