@@ -318,6 +318,10 @@ typedef struct vae2_bn_layer {
   float* rpartials;               /* backward reduce: [2][vae2_bn_partial_rows(xd)][c]  */
   const double* rsums;            /* backward apply: the residual BN's [2][c] sums       */
   float* rdx; vae2_act rdxd;      /* backward apply: the residual BN's input gradient   */
+  /* ABI 10: the ReLU mask as one byte per (pixel, channel quad), bit k = (y[4q+k] > 0),
+   * [P][ceil(c/4)]: written by vae2_bn_multi_apply when non-NULL, read by the backward
+   * passes instead of y (a) -- 1/16 of y's bytes.  NULL: y / recomputed from x.         */
+  unsigned char* mask;
 } vae2_bn_layer;
 /* y = relu?(fma(x, scale, shift) + a) per layer (vae2_bn_apply).                 */
 int vae2_bn_multi_apply(int n, const vae2_bn_layer* layers, void* stream);

@@ -31,6 +31,7 @@ def _blocks(seed, chans):
 def _run(lazy, seed, chans, shapes, monkeypatch):
     from vae2 import hrnet, ops
     monkeypatch.setattr(ops, "LAZY_BN", lazy)
+    monkeypatch.setattr(ops, "MASK_BYTES", lazy)  # bn2's ReLU mask as bytes vs y
     made = []
     real = ops.LazyBN
 
@@ -164,6 +165,7 @@ def _bottleneck_run(flags, monkeypatch, shape=(2, 64, 128), seed=3):
     lazy, resbn = flags
     monkeypatch.setattr(ops, "LAZY_BN", lazy)
     monkeypatch.setattr(ops, "RES_BN", resbn)
+    monkeypatch.setattr(ops, "MASK_BYTES", resbn)
     torch.manual_seed(seed)
     blk = hrnet.make_layer(hrnet.Bottleneck, 64, 64, 2).to(DEV)
     for m in blk.modules():
@@ -188,9 +190,9 @@ def _bottleneck_run(flags, monkeypatch, shape=(2, 64, 128), seed=3):
 @pytest.mark.parametrize("shape", [(2, 64, 128), (3, 40, 72)])
 def test_resbn_shortcut_equals_stored(shape, monkeypatch):
     """ops.ResBN (the Bottleneck's downsample BN added inside bn3's apply, its partials and
-    input gradient from bn3's backward kernels) and the Bottleneck's LazyBN bn1 against the
-    stored path: forward bit-identical, gradients and running statistics within fp32
-    summation-order noise."""
+    input gradient from bn3's backward kernels), the Bottleneck's LazyBN bn1 and bn3's ReLU
+    mask bytes against the stored path: forward bit-identical, gradients and running
+    statistics within fp32 summation-order noise."""
     ba, xa, ya = _bottleneck_run((True, True), monkeypatch, shape)
     bb, xb, yb = _bottleneck_run((False, False), monkeypatch, shape)
     assert torch.equal(ya, yb)

@@ -580,6 +580,9 @@ struct BnLayer {
   const double* rsums;
   float* rdx;
   int rx_ps, rdx_ps;
+  // ReLU mask, one byte per (pixel, channel quad) (bit k: channel 4q+k > 0): written by the
+  // forward apply, read by the backward passes instead of y (1/16 of y's bytes)
+  uint8_t* mk;
 };
 
 struct BnMulti {
@@ -626,6 +629,9 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
       o[k] = (L.relu && t < 0.f) ? 0.f : t;  // NaN propagates (torch.relu)
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
+    if (L.mk)  // threshold_backward's test (y > 0: NaN and 0 cut the gradient)
+      L.mk[p * c4 + (c >> 2)] = (uint8_t)((o[0] > 0.f) | ((o[1] > 0.f) << 1) |
+                                          ((o[2] > 0.f) << 2) | ((o[3] > 0.f) << 3));
   }
 }
 
@@ -644,7 +650,8 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
   if (p1 > L.P) p1 = L.P;
   f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s0;
   const int r = tid / c4, c = 4 * (tid - r * c4);
-  const float* y = L.relu ? L.a : nullptr;
+  const uint8_t* mk = L.relu ? L.mk : nullptr;  // stored mask, else y, else from x
+  const float* y = L.relu && !mk ? L.a : nullptr;
   const bool rb = L.rx != nullptr;  // + the residual BN's sum g * xhat_r (same g)
   if (tid < L.rows * c4) {
     const f4 mean = chan4(L.save, c, C), invstd = chan4(L.save + C, c, C);
@@ -655,6 +662,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
     // same accumulation order as one pixel at a time)
     for (int64_t pb = p0 + r; pb < p1; pb += (int64_t)kApplyU * L.rows) {
       f4 xv[kApplyU], gv[kApplyU], yv[kApplyU], rv[kApplyU];
+      uint32_t mv[kApplyU];
 #pragma unroll
       for (int u = 0; u < kApplyU; ++u) {
         const int64_t p = pb + u * L.rows;
@@ -662,6 +670,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
           xv[u] = ld4(L.x + p * L.x_ps + c);
           gv[u] = ld4(L.dy + p * L.dy_ps + c);
           if (y) yv[u] = ld4(y + p * L.a_ps + c);
+          if (mk) mv[u] = mk[p * c4 + (c >> 2)];
           if (rb) rv[u] = ld4(L.rx + p * L.rx_ps + c);
         }
       }
@@ -672,7 +681,8 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
         f4 ga = gv[u];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if (L.relu && !((y ? yv[u][k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f))
+          if (L.relu && !(mk ? ((mv[u] >> k) & 1u) != 0
+                             : (y ? yv[u][k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f))
             ga[k] = 0.f;
           s0[k] += ga[k];
           s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
@@ -726,7 +736,8 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   const int r = tid / c4, c = 4 * (tid - r * c4);
   const double count = L.countp ? *L.countp : L.count;
   const float inv_n = (float)(1.0 / count);
-  const float* y = L.relu ? L.a : nullptr;
+  const uint8_t* mk = L.relu ? L.mk : nullptr;  // stored mask, else y, else from x
+  const float* y = L.relu && !mk ? L.a : nullptr;
   const bool rb = L.rx != nullptr;
   f4 mean, invstd, sc, sh, mg, mgx, k4;
   f4 rmean = {0.f, 0.f, 0.f, 0.f}, rinv = rmean, rmg = rmean, rmgx = rmean, rk4 = rmean;
@@ -750,6 +761,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   }
   const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
   f4 gv[kApplyU], xv[kApplyU], yv[kApplyU], rxv[kApplyU];
+  uint32_t mv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
     const int64_t p = pb + u * L.rows;
@@ -757,6 +769,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
       gv[u] = ld4(L.dy + p * L.dy_ps + c);
       xv[u] = ld4(L.x + p * L.x_ps + c);
       if (y) yv[u] = ld4(y + p * L.a_ps + c);
+      if (mk) mv[u] = mk[p * c4 + (c >> 2)];
       if (rb) rxv[u] = ld4(L.rx + p * L.rx_ps + c);
     }
   }
@@ -767,7 +780,9 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
     f4 g = gv[u], o;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (L.relu && !((y ? yv[u][k] : __builtin_fmaf(xv[u][k], sc[k], sh[k])) > 0.f)) g[k] = 0.f;
+      if (L.relu && !(mk ? ((mv[u] >> k) & 1u) != 0
+                         : (y ? yv[u][k] : __builtin_fmaf(xv[u][k], sc[k], sh[k])) > 0.f))
+        g[k] = 0.f;
       const float xh = (xv[u][k] - mean[k]) * invstd[k];
       o[k] = k4[k] * (g[k] - mg[k] - xh * mgx[k]);
     }
@@ -1170,6 +1185,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       L.rx = l.rx; L.rsave = l.rsave; L.rgamma = l.rgamma; L.rpart = l.rpartials;
       L.rsums = l.rsums; L.rdx = l.rdx;
       L.rx_ps = (int)l.rxd.ps; L.rdx_ps = (int)l.rdxd.ps;
+      L.mk = l.mask;
       L.rows = quad_rows(l.xd.c);
       L.blk0 = blocks;
       if (kind == 1) {

@@ -35,7 +35,8 @@ class BnLayer(ctypes.Structure):
                 ("save", c_vp), ("gamma", c_vp), ("partials", c_vp), ("sums", c_vp),
                 ("countp", c_vp), ("count", c_f64), ("relu", c_int), ("dres_acc", c_int),
                 ("rx", c_vp), ("rxd", Act), ("rsave", c_vp), ("rgamma", c_vp),
-                ("rpartials", c_vp), ("rsums", c_vp), ("rdx", c_vp), ("rdxd", Act)]
+                ("rpartials", c_vp), ("rsums", c_vp), ("rdx", c_vp), ("rdxd", Act),
+                ("mask", c_vp)]
 
 
 class BnFin(ctypes.Structure):

@@ -167,6 +167,7 @@ class ResBN:
 
 
 RES_BN = True  # False: the shortcut BN output is stored (A/B and parity tests)
+MASK_BYTES = True  # residual layers keep their ReLU mask as bytes for the backward (vs y)
 
 
 def lazy_bn_ok(shape, conv):
@@ -773,6 +774,7 @@ class _ConvBNMulti(torch.autograd.Function):
             vdist.all_reduce_(buf, group=group)
             call("vae2_bn_multi_finalize", n, arr, s)
         ys, lay = [], []
+        masks = [None] * n
         for i, (r, save, spec) in enumerate(zip(rs, saves, specs)):
             lz = spec.bn_out
             if isinstance(lz, ResBN):  # added by its consumer's apply: r stands in for y
@@ -787,6 +789,14 @@ class _ConvBNMulti(torch.autograd.Function):
             res = L[i][5]
             layer = _bn_layer(r, res, y, None, None, save, None, None, None, None, 0.0,
                               spec.relu)
+            if MASK_BYTES and spec.relu and (res is not None or spec.res_bn is not None):
+                # the backward's ReLU mask (it cannot be recomputed from r): 1 byte per
+                # channel quad instead of re-reading y twice
+                _, ya_ = act_of(y)
+                mk = torch.empty((ya_.n * ya_.h * ya_.w * ((ya_.c + 3) // 4),),
+                                 dtype=torch.uint8, device=y.device)
+                layer.mask = mk.data_ptr()
+                masks[i] = mk
             if spec.res_bn is not None:
                 j = spec.res_bn
                 layer.rx, layer.rxd = rs[j].data_ptr(), act_of(rs[j])[1]
@@ -796,9 +806,12 @@ class _ConvBNMulti(torch.autograd.Function):
             if prof.active():
                 prof.note(0, sum(4.0 * r.numel() * (3 if L[i][5] is not None or
                                                     specs[i].res_bn is not None else 2)
-                                 for i, r in enumerate(rs) if specs[i].bn_out is None))
+                                 for i, r in enumerate(rs) if specs[i].bn_out is None),
+                          _bn_label("bn apply", [rs[i] for i in range(n)
+                                                 if specs[i].bn_out is None]))
             call("vae2_bn_multi_apply", len(lay), (_lib.BnLayer * len(lay))(*lay), s)
         ctx.specs = specs
+        ctx.masks = masks
         ctx.counts = counts
         ctx.group = group
         ctx.has_res = [l_[5] is not None for l_ in L]
@@ -880,9 +893,12 @@ class _ConvBNMulti(torch.autograd.Function):
             bsink, bret = _grad_sink(beta, need[1 + 6 * i + 4])
             sums_p = buf.data_ptr() + 8 * off
             countp = buf.data_ptr() + 8 * (tot + i) if group is not None else None
-            lay[i] = _bn_layer(r, y if ctx.has_res[i] or spec.res_bn is not None else None, dr,
-                               dy, dres, save, gamma, part, sums_p, countp, ctx.counts[i],
-                               spec.relu, acc)
+            mk = ctx.masks[i]
+            lay[i] = _bn_layer(r, y if (ctx.has_res[i] or spec.res_bn is not None) and mk is None
+                               else None, dr, dy, dres, save, gamma, part, sums_p, countp,
+                               ctx.counts[i], spec.relu, acc)
+            if mk is not None:
+                lay[i].mask = mk.data_ptr()
             if spec.res_bn is not None:  # the shortcut BN's passes ride on this layer's
                 j = spec.res_bn
                 rpart, _, rdr, rsums_p = resbuf[j]
@@ -900,9 +916,9 @@ class _ConvBNMulti(torch.autograd.Function):
             off += 2 * cs[i]
         if red:
             if prof.active():
-                prof.note(0, sum(4.0 * rs[i].numel() * (2 + (1 if ctx.has_res[i] else 0) +
-                                                        (2 if specs[i].res_bn is not None else 0))
-                                 for i in red))
+                prof.note(0, sum(4.0 * rs[i].numel() * (2 + _y_reads(ctx, i) +
+                                                        (1 if specs[i].res_bn is not None else 0))
+                                 for i in red), _bn_label("bn bwd reduce", [rs[i] for i in red]))
             call("vae2_bn_multi_bwd_reduce", len(red), (_lib.BnLayer * len(red))(*[lay[i] for i in red]),
                  s)
         call("vae2_bn_multi_reduce", n, fins, 1, s)  # local sums + dgamma / dbeta
@@ -910,10 +926,10 @@ class _ConvBNMulti(torch.autograd.Function):
             from . import dist as vdist
             vdist.all_reduce_(buf, group=group)
         if prof.active():
-            prof.note(0, sum(4.0 * rs[i].numel() * (3 + (1 if ctx.has_res[i] else 0) +
+            prof.note(0, sum(4.0 * rs[i].numel() * (3 + _y_reads(ctx, i) +
                                                     (1 if dress[i][0] is not None else 0) +
-                                                    (3 if specs[i].res_bn is not None else 0))
-                             for i in act))
+                                                    (2 if specs[i].res_bn is not None else 0))
+                             for i in act), _bn_label("bn bwd apply", [rs[i] for i in act]))
         call("vae2_bn_multi_bwd_apply", len(act), (_lib.BnLayer * len(act))(*[lay[i] for i in act]),
              s)
         grads = [None]
@@ -943,6 +959,20 @@ class _ConvBNMulti(torch.autograd.Function):
 
 def _p(t):
     return t.data_ptr() if t is not None else None
+
+
+def _y_reads(ctx, i):
+    """Bytes (in units of the layer's fp32 tensor) a backward pass reads for the ReLU mask:
+    y, its byte mask (1/16), or nothing (recomputed from r)."""
+    if ctx.masks[i] is not None:
+        return 1.0 / 16.0
+    return 1 if ctx.has_res[i] or ctx.specs[i].res_bn is not None else 0
+
+
+def _bn_label(kind, rs):
+    """Profiler row label of a multi-layer BN launch: its layers' C@HxW (N in the bytes)."""
+    return f"{kind} " + " + ".join(f"{int(r.shape[3])}@{int(r.shape[1])}x{int(r.shape[2])}"
+                                   for r in rs)
 
 
 def _aligned_copy(t):
