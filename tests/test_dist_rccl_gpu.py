@@ -70,12 +70,12 @@ def _work(port, q):
     # the early buckets read the decoders' tail when the x2t_hat hook fired (after the
     # flush of the queued dW reductions and the side-stream join): nothing the rest of the
     # backward ran may write it afterwards (at world 1 the all-reduce is an identity)
-    tail_final = (len(vdist.EARLY_CHECK) >= 1 and
-                  all(torch.equal(b[s:], snap) for b, s, snap in vdist.EARLY_CHECK))
+    tail_final = (len(vdist.EARLY_CHECK) >= 2 and  # the decoders' tail + the posterior net
+                  all(torch.equal(b[lo:hi], snap) for b, lo, hi, snap in vdist.EARLY_CHECK))
     vdist.EARLY_CHECK = None
     # the decoders' buckets were started from the x2t_hat hook during backward
-    early = {k: (v[0], len(v[1])) for k, v in vdist._EARLY.items()}
-    ed_flat = opt.flats[1]
+    early = {k: [(lo, hi, len(w)) for lo, hi, w in v] for k, v in vdist._EARLY.items()}
+    ez_flat, ed_flat = opt.flats
     vdist.allreduce_grads(opt.flats)
     red = vdist.reduce_tensor(loss.detach().clone())
     torch.cuda.synchronize()
@@ -86,8 +86,10 @@ def _work(port, q):
     fwd_same = got[0] == ref[0] and np.array_equal(got[1], ref[1])
     grad_rel = float((got[2] - ref[2]).norm() / ref[2].norm())
     grad_same = bool(torch.equal(got[2], ref[2]))
-    early_ok = (early.get(id(ed_flat), (None, 0))[0] == vdist.tail_range(ed_flat) and
-                early[id(ed_flat)][1] >= 1)
+    early_ok = (any(lo == vdist.tail_range(ed_flat) and n >= 1
+                    for lo, hi, n in early.get(id(ed_flat), [])) and
+                any(lo == 0 and hi == ez_flat.grad.numel() and n >= 1
+                    for lo, hi, n in early.get(id(ez_flat), [])))
     q.put(("ok", got[0], float(red), float(g["loss_loss_all"]), fwd_same, grad_rel, exchanges,
            base_same, grad_same, early_ok, tail_final))
     dist.destroy_process_group()
@@ -123,8 +125,8 @@ def test_rccl_world1_dist_path_equals_single_process_step():
     assert abs(loss - ref) <= 1e-5 * abs(ref)
     assert reduced == loss
     assert exchanges > 50  # SyncBN statistics went through RCCL
-    assert early_ok, "the decoders' gradient buckets did not start during backward"
-    assert tail_final, "the decoders' gradient tail changed after its buckets started"
+    assert early_ok, "the decoders' / posterior's gradient buckets did not start during backward"
+    assert tail_final, "a gradient range changed after its buckets started"
     assert fwd_same, "the RCCL path changed the forward"
     if base_same:  # a deterministic step must stay bit-identical through the RCCL path
         assert grad_same, grad_rel

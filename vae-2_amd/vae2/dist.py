@@ -111,26 +111,67 @@ def tail_range(flat, prefixes=("decf_", "decp_")):
     return flat.offsets[idx[0]]
 
 
+def _start_range(flat, lo, hi):
+    """Flush the queued weight-gradient reductions, join the side streams, then start the
+    bucketed all-reduce of flat.grad[lo:hi] (recorded in _EARLY for allreduce_grads)."""
+    ops.flush_wgrad()   # queued weight-gradient reductions (they write the range)
+    streams.join_all()  # side-stream work (the posterior net, the past decoder)
+    buf = flat.grad
+    if EARLY_CHECK is not None:  # the range as the buckets see it (no later write allowed)
+        EARLY_CHECK.append((buf, lo, hi, buf[lo:hi].clone()))
+    works = [dist.all_reduce(buf[off:min(off + BUCKET_ELEMS, hi)], group=grad_group(),
+                             async_op=True)
+             for off in range(lo, hi, BUCKET_ELEMS)]
+    _EARLY.setdefault(id(flat), []).append((lo, hi, works))
+
+
+def _overlap_ok():
+    return OVERLAP and is_dist() and dist.get_backend(grad_group()) != "gloo"
+
+
 def early_reduce_hook(t, flat, start):
     """Start the all-reduce of flat.grad[start:] when t's gradient is complete."""
-    if not (OVERLAP and is_dist() and t.requires_grad and start is not None):
-        return
-    if dist.get_backend(grad_group()) == "gloo":
-        return  # host-staged gloo reduces synchronously: nothing to overlap
+    if not (_overlap_ok() and t.requires_grad and start is not None):
+        return  # (host-staged gloo reduces synchronously: nothing to overlap)
 
     def hook(g):
-        ops.flush_wgrad()   # the decoders' queued weight-gradient reductions
-        streams.join_all()  # the decoders' side-stream work
-        buf = flat.grad
-        if EARLY_CHECK is not None:  # the tail as the buckets see it (no later write allowed)
-            EARLY_CHECK.append((buf, start, buf[start:].clone()))
-        works = [dist.all_reduce(buf[off:off + BUCKET_ELEMS], group=grad_group(),
-                                 async_op=True)
-                 for off in range(start, buf.numel(), BUCKET_ELEMS)]
-        _EARLY[id(flat)] = (start, works)
+        _start_range(flat, start, flat.grad.numel())
         return g
 
     t.register_hook(hook)
+
+
+class _Anchor(torch.autograd.Function):
+    """Identity on x whose backward runs once the gradient of every op that consumed x is
+    complete -- i.e. after the whole sub-network x feeds: starts that network's gradient
+    buckets then (x itself need not require grad; the anchor tensor does)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, flat, lo, hi):
+        ctx.args = (flat, lo, hi)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gx, *_):
+        flat, lo, hi = ctx.args
+        _start_range(flat, lo, hi)
+        return gx, None, None, None, None
+
+
+_ANCHOR = {}
+
+
+def anchor_reduce(x, flat, lo=0, hi=None):
+    """x, routed so that flat.grad[lo:hi] is all-reduced (async) as soon as the backward
+    of the sub-network fed by x is done: the posterior net's buckets start while the
+    encoder's backward still runs (its trunk is the deepest part of the step)."""
+    if flat is None or not _overlap_ok() or not torch.is_grad_enabled():
+        return x
+    dev = x.device
+    a = _ANCHOR.get(dev)
+    if a is None:
+        a = _ANCHOR[dev] = torch.zeros((), device=dev, requires_grad=True)
+    return _Anchor.apply(x, a, flat, lo, flat.grad.numel() if hi is None else hi)
 
 
 def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
@@ -142,14 +183,22 @@ def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
     pending = []
     for f in flats:
         g = f.grad
-        start, works = _EARLY.pop(id(f), (g.numel(), []))
-        head = g[:start]
-        if dist.get_backend(grad_group()) == "gloo":
-            bucket_allreduce(head, bucket_elems, group=grad_group())
-        else:
-            works = [dist.all_reduce(head[off:off + bucket_elems], group=grad_group(),
-                                     async_op=True)
-                     for off in range(0, head.numel(), bucket_elems)] + works
+        done = sorted(_EARLY.pop(id(f), []))
+        works, gaps, pos = [], [], 0
+        for lo, hi, w in done:  # the ranges no hook started yet
+            if lo > pos:
+                gaps.append((pos, lo))
+            pos = max(pos, hi)
+            works += w
+        if pos < g.numel():
+            gaps.append((pos, g.numel()))
+        for lo, hi in gaps:
+            if dist.get_backend(grad_group()) == "gloo":
+                bucket_allreduce(g[lo:hi], bucket_elems, group=grad_group())
+            else:
+                works += [dist.all_reduce(g[off:min(off + bucket_elems, hi)], group=grad_group(),
+                                          async_op=True)
+                          for off in range(lo, hi, bucket_elems)]
         pending.append((g, works))
     for g, works in pending:
         for w in works:

@@ -625,6 +625,8 @@ class HighResolutionNetEDz(HighResolutionNet):
 
     def run(self, x):
         """x: (N,H,W,6L) NHWC -> (N,1,1,2z) or, with HD_Z, a list of (N,h_b,w_b,2z)."""
+        # its gradient buckets start as soon as its backward is done (vae2.dist)
+        x = vdist.anchor_reduce(x, getattr(self, "_vae2_flat", None))
         xs = self._trunk_to_stage4_inputs("", x)
         ys = run_stage(self.stage4, xs)
         if self.hd_z:
