@@ -85,6 +85,8 @@ def parse():
                          "(vae2.ops.LazyBN; A/B)")
     ap.add_argument("--conv-algo", type=int, default=None,
                     help="vae2_conv2d_set_algo bits (A/B of kernel choices; default: auto)")
+    ap.add_argument("--conv-tune", default="",
+                    help="vae2_conv2d_set_tune key=value[,key=value] (launch-shape A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
     ap.add_argument("--full-step", action="store_true",
@@ -244,6 +246,10 @@ def main():
     if args.conv_algo is not None:
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_algo(args.conv_algo)
+    for kv in filter(None, args.conv_tune.split(",")):
+        from vae2 import _lib
+        k, v = kv.split("=")
+        _lib.load().vae2_conv2d_set_tune(int(k), int(v))
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False

@@ -70,6 +70,10 @@ int vae2_conv2d_set_algo(int algo);
  * rounded to bf16 (RNE) as they enter the MFMA; accumulation, storage, BatchNorm and the
  * optimizer stay fp32).  Returns the previous setting.  Process-wide.             */
 int vae2_conv2d_set_mfma_bf16(int on);
+/* Launch-shape tuning knobs for A/B measurements (every setting computes the same
+ * result): key 0 = minimum igemm workgroups (row tiles shrink 4 -> 2 -> 1 until the grid
+ * reaches it; 0 = the default rule).  Returns the previous value, -1 for an unknown key. */
+int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
  * reduction (one process-wide queue); vae2_wgrad_flush launches the queued reductions

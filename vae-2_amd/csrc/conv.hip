@@ -1177,9 +1177,10 @@ int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU rema
 int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persistent 1x1 GEMM
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
 int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
+int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide;
+    g_dconv_nr_wide, g_igemm_minblk;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1213,6 +1214,11 @@ static Tile pick_tile(int64_t M, int N, bool wide = false) {
 static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   const bool wide = wide_ok(M, N, taps);
   Tile t = pick_tile(M, N, wide);
+  // smaller row tiles until the grid reaches g_igemm_minblk workgroups (more waves per
+  // SIMD for layers whose 4-row-tile grid leaves one wave per SIMD)
+  while (!wide && g_igemm_minblk > 0 && t.tm > 1 &&
+         ceil_div(M, 64 * t.tm) * t.nblk * ncls < g_igemm_minblk)
+    t.tm >>= 1;
   const int64_t blocks = ceil_div(M, 64 * t.tm) * t.nblk * ncls;
   const int chunks = (taps * k4 + 15) / 16;
   if (g_ksplit && !wide && blocks < 512 && chunks >= 16) t.ks = 4;
@@ -2386,6 +2392,18 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
   VAE2_LAUNCH(pack_weights_batched_kernel, dim3(32, (unsigned)njobs), dim3(256), 0,
                      as_stream(stream), jobs);
   return check_launch(fn);
+}
+
+// Launch-shape tuning knobs (A/B measurements; every setting computes the same result):
+// key 0 = igemm minimum workgroups (0: the default row-tile rule).  Returns the previous
+// value, or -1 for an unknown key.
+int vae2_conv2d_set_tune(int key, int value) {
+  if (key == 0) {
+    const int prev = g_igemm_minblk;
+    g_igemm_minblk = value < 0 ? 0 : value;
+    return prev;
+  }
+  return -1;
 }
 
 int vae2_conv2d_set_mfma_bf16(int on) {

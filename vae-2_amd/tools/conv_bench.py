@@ -72,6 +72,7 @@ def main():
                     help="vae2_conv2d_set_algo values to compare (0 auto, 1 gather, 2 direct)")
     ap.add_argument("--all", action="store_true", help="every ELBO conv shape (ALL_SHAPES)")
     ap.add_argument("--bf16", action="store_true", help="bf16 MFMA operands")
+    ap.add_argument("--tune", default="", help="vae2_conv2d_set_tune key=value[,key=value]")
     a = ap.parse_args()
     if a.all:
         SHAPES[:] = ALL_SHAPES
@@ -80,6 +81,9 @@ def main():
     for _ in range(200):  # bring the clocks up before the first timed shape
         warm = warm @ warm.T * 1e-4
     torch.cuda.synchronize()
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        lib.vae2_conv2d_set_tune(int(k), int(v))
     for algo in a.algo:
         lib.vae2_conv2d_set_algo(algo)
         lib.vae2_conv2d_set_mfma_bf16(1 if a.bf16 else 0)

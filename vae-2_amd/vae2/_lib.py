@@ -59,6 +59,7 @@ _SIGS = {
     "vae2_conv2d_pack_weights": (c_int, [c_vp, c_i64, c_vp]),
     "vae2_conv2d_fwd_stats_rows": (c_i64, [c_vp, P_ACT, P_ACT, c_int, c_int, c_int]),
     "vae2_conv2d_set_mfma_bf16": (c_int, [c_int]),
+    "vae2_conv2d_set_tune": (c_int, [c_int, c_int]),
     "vae2_wgrad_defer": (c_int, [c_int]),
     "vae2_wgrad_flush": (c_int, [c_vp]),
     "vae2_conv2d_set_algo": (c_int, [c_int]),
