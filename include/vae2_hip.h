@@ -417,6 +417,12 @@ int vae2_upsample_bilinear_bwd(const float* dy, const vae2_act* dyd, float* dx,
  * are bilinearly upsampled (HighResolutionModule fuse, enc_hrnet.py:233-249). */
 int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
                        float* y, const vae2_act* yd, void* stream);
+/* ABI 10: as vae2_fuse_sum_relu, with saves[i] (or NULL) the BatchNorm [4][c] (mean,
+ * invstd, scale, shift) of term i: x_i is then that BN's pre-BN input r and the term is
+ * fma(r, scale, shift) (the fuse unit's BN output, enc_hrnet.py:199-218, never stored). */
+int vae2_fuse_sum_relu_bn(int n, const float* const* xs, const vae2_act* xds,
+                          const float* const* saves, float* y, const vae2_act* yd,
+                          void* stream);
 
 /* Head-kernel variants (A/B measurement): bit 0 = the per-channel-lane vertical pass of
  * the power-of-two upsampling adjoint instead of the row-streaming one; bit 1 = the

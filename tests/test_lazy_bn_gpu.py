@@ -202,3 +202,49 @@ def test_resbn_shortcut_equals_stored(shape, monkeypatch):
     for (na, ra), (_, rb_) in zip(ba.named_buffers(), bb.named_buffers()):
         if "running" in na:
             assert torch.equal(ra, rb_), na
+
+
+def _module_run(fuse_lazy, monkeypatch, seed=4):
+    """A W18 stage-4 HighResolutionModule (4 branches, 2 BasicBlocks each, fuse rows with up
+    paths and down chains) at 32x64, B=2, training BN."""
+    from helpers import build, make_cfg
+    from vae2 import ops
+    monkeypatch.setattr(ops, "FUSE_LAZY", fuse_lazy)
+    ed, _ = build(make_cfg(arch="w18", hw=(32, 64)))
+    mod = ed.stage4[0].to(DEV)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in mod.modules():
+            if isinstance(m, nn.Conv2d):
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) / m.weight[0].numel() ** 0.5)
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.copy_(1.0 + 0.3 * torch.randn(m.weight.shape, generator=g))
+                m.bias.copy_(0.3 * torch.randn(m.bias.shape, generator=g))
+    xs = []
+    for c, h, w in [(18, 32, 64), (36, 16, 32), (72, 8, 16), (144, 4, 8)]:
+        x = ops.new_act((2, h, w, c), torch.empty(1, device=DEV))
+        with torch.no_grad():
+            x.copy_(torch.randn(x.shape, generator=g).to(DEV))
+        xs.append(x.requires_grad_(True))
+    ys = mod.run(xs)
+    gs = [torch.randn(y.shape, generator=g).to(DEV) for y in ys]
+    torch.autograd.backward(ys, gs)
+    torch.cuda.synchronize()
+    return mod, xs, ys
+
+
+def test_fuse_lazy_units_equal_stored(monkeypatch):
+    """The fuse units' BN outputs formed inside the fuse sum (ops.fuse_sum_relu lazies:
+    vae2_fuse_sum_relu_bn) against the stored path: outputs bit-identical, input / weight
+    / BN gradients within summation-order noise, running statistics identical."""
+    ma, xa, ya = _module_run(True, monkeypatch)
+    mb, xb, yb = _module_run(False, monkeypatch)
+    for u, v in zip(ya, yb):
+        assert torch.equal(u, v)
+    for u, v in zip(xa, xb):
+        assert rel_nz(u.grad, v.grad) < 1e-5
+    for (n, p), (_, q) in zip(ma.named_parameters(), mb.named_parameters()):
+        assert rel_nz(p.grad, q.grad) < 1e-5, n
+    for (n, a), (_, b) in zip(ma.named_buffers(), mb.named_buffers()):
+        if "running" in n:
+            assert torch.equal(a, b), n

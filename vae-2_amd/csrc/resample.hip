@@ -300,8 +300,18 @@ __global__ __launch_bounds__(256) void up_adjq_kernel(UpAdjQ p) {
 struct FuseTerms {
   const float* x[4];
   Act d[4];
+  const float* sv[4];  // BatchNorm (mean, invstd, scale, shift) applied to the term, or null
   int n;
 };
+
+// A term that is the pre-BN output r of a BatchNorm layer whose normalised output is never
+// stored (a fuse unit's conv + BN, enc_hrnet.py:199-218): its values are fma(r, scale,
+// shift) -- bn_apply's arithmetic, so the sum is the stored path's bit for bit.
+__device__ __forceinline__ float term_at(const float* x, const float* sv, int64_t i, int c,
+                                         int C) {
+  const float v = x[i];
+  return sv ? __builtin_fmaf(v, sv[2 * C + c], sv[3 * C + c]) : v;
+}
 
 __global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* __restrict__ y,
                                                             Act yd, FastDiv cdiv, FastDiv wdiv,
@@ -321,12 +331,23 @@ __global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* 
     for (int k = 0; k < 4; ++k) {
       if (k >= t.n) break;
       const Act& d = t.d[k];
+      const float* sv = t.sv[k];
       float v;
-      if (d.h == yd.h && d.w == yd.w)
-        v = t.x[k][(int64_t)p * d.ps + c];
-      else
+      if (d.h == yd.h && d.w == yd.w) {
+        v = term_at(t.x[k], sv, (int64_t)p * d.ps + c, (int)c, (int)C);
+      } else if (!sv) {
         v = bilinear_at(t.x[k], d, n, oy, ox, c, (float)d.h / (float)yd.h,
                         (float)d.w / (float)yd.w);
+      } else {  // bilinear_at of the normalised taps
+        const Lerp ly = lerp_index(oy, (int)d.h, (float)d.h / (float)yd.h);
+        const Lerp lx = lerp_index(ox, (int)d.w, (float)d.w / (float)yd.w);
+        const float* base = t.x[k] + (int64_t)n * d.h * d.w * d.ps;
+        const float x00 = term_at(base, sv, ((int64_t)ly.i0 * d.w + lx.i0) * d.ps + c, (int)c, (int)C);
+        const float x01 = term_at(base, sv, ((int64_t)ly.i0 * d.w + lx.i1) * d.ps + c, (int)c, (int)C);
+        const float x10 = term_at(base, sv, ((int64_t)ly.i1 * d.w + lx.i0) * d.ps + c, (int)c, (int)C);
+        const float x11 = term_at(base, sv, ((int64_t)ly.i1 * d.w + lx.i1) * d.ps + c, (int)c, (int)C);
+        v = ly.l0 * (lx.l0 * x00 + lx.l1 * x01) + ly.l1 * (lx.l0 * x10 + lx.l1 * x11);
+      }
       acc = (k == 0) ? v : acc + v;
     }
     y[(int64_t)p * yd.ps + c] = acc < 0.f ? 0.f : acc;  // NaN propagates (torch.relu)
@@ -666,9 +687,9 @@ int vae2_upsample_bilinear_bwd_pow2(const float* dy, const vae2_act* dyd, int n,
   return check_launch(fn);
 }
 
-int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
-                       float* y, const vae2_act* yd, void* stream) {
-  const char* fn = "vae2_fuse_sum_relu";
+static int fuse_sum_relu_impl(int n, const float* const* xs, const vae2_act* xds,
+                              const float* const* saves, float* y, const vae2_act* yd,
+                              void* stream, const char* fn) {
   VAE2_REQUIRE(n >= 1 && n <= 4 && xs && xds && y && act_ok(yd), fn, "bad arguments");
   FuseTerms t{};
   t.n = n;
@@ -678,6 +699,7 @@ int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
     VAE2_REQUIRE(xds[k].h <= yd->h && xds[k].w <= yd->w, fn, "terms cannot be downsampled");
     t.x[k] = xs[k];
     t.d[k] = to_act(&xds[k]);
+    t.sv[k] = saves ? saves[k] : nullptr;
   }
   int64_t total = act_elems(yd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
@@ -685,6 +707,17 @@ int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
                      as_stream(stream), t, y, to_act(yd), FastDiv((uint32_t)yd->c),
                      FastDiv((uint32_t)yd->w), FastDiv((uint32_t)yd->h));
   return check_launch(fn);
+}
+
+int vae2_fuse_sum_relu(int n, const float* const* xs, const vae2_act* xds,
+                       float* y, const vae2_act* yd, void* stream) {
+  return fuse_sum_relu_impl(n, xs, xds, nullptr, y, yd, stream, "vae2_fuse_sum_relu");
+}
+
+int vae2_fuse_sum_relu_bn(int n, const float* const* xs, const vae2_act* xds,
+                          const float* const* saves, float* y, const vae2_act* yd,
+                          void* stream) {
+  return fuse_sum_relu_impl(n, xs, xds, saves, y, yd, stream, "vae2_fuse_sum_relu_bn");
 }
 
 int vae2_relu_bwd(const float* dy, const vae2_act* dyd, const float* y,

@@ -119,6 +119,8 @@ _SIGS = {
     "vae2_upsample_bilinear_fwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
     "vae2_upsample_bilinear_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_f32, c_vp]),
     "vae2_fuse_sum_relu": (c_int, [c_int, ctypes.POINTER(c_vp), P_ACT, c_vp, P_ACT, c_vp]),
+    "vae2_fuse_sum_relu_bn": (c_int, [c_int, ctypes.POINTER(c_vp), P_ACT, ctypes.POINTER(c_vp),
+                                      c_vp, P_ACT, c_vp]),
     "vae2_relu_bwd_dual": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_f32,
                                    c_vp]),
     "vae2_relu_bwd": (c_int, [c_vp, P_ACT, c_vp, P_ACT, c_vp, P_ACT, c_vp]),

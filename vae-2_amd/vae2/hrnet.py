@@ -124,13 +124,14 @@ def _run_convbn_seq(seq, x, x_link=None):
     return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2, x_link=x_link)
 
 
-def _run_convbn_seqs(seqs, xs, x_links=None):
+def _run_convbn_seqs(seqs, xs, x_links=None, bn_outs=None):
     """Independent Sequential(Conv2d, BatchNorm2d[, ReLU]) units of one depth level,
-    their BatchNorm steps in shared launches (ops.conv_bn_multi)."""
+    their BatchNorm steps in shared launches (ops.conv_bn_multi).  bn_outs: per unit a
+    LazyBN whose output is handed over un-normalised (set to None where it is stored)."""
     if not seqs:
         return []
     return ops.conv_bn_multi(xs, [q[0] for q in seqs], [q[1] for q in seqs],
-                             [len(q) > 2 for q in seqs], x_links=x_links)
+                             [len(q) > 2 for q in seqs], x_links=x_links, bn_outs=bn_outs)
 
 
 def run_blocks_lockstep(blocks, xs):
@@ -252,26 +253,35 @@ class HighResolutionModule(nn.Module):
         # (ops.GradLink) instead of autograd add kernels.
         rows = list(enumerate(self.fuse_layers))
         links = [ops.GradLink(len(rows)) if len(rows) > 1 else None for _ in range(nb)]
-        terms = {}
+        # the units feeding a fuse sum (every up path, the last unit of every down chain)
+        # hand over their pre-BN output: the fuse kernel normalises it (ops.fuse_sum_relu
+        # lazies), so their BN apply pass never runs and the output is never stored
+        terms, lazy = {}, {}
         ups = [(i, j) for i, _ in rows for j in range(nb) if j > i]
-        for (i, j), t in zip(ups, _run_convbn_seqs([self.fuse_layers[i][j] for i, j in ups],
-                                                  [xs[j] for _, j in ups],
-                                                  [links[j] for _, j in ups])):
-            terms[(i, j)] = t
+        lz_up = [ops.LazyBN() if ops.FUSE_LAZY else None for _ in ups]
+        for (i, j), t, lz in zip(ups, _run_convbn_seqs([self.fuse_layers[i][j] for i, j in ups],
+                                                       [xs[j] for _, j in ups],
+                                                       [links[j] for _, j in ups], lz_up),
+                                 lz_up):
+            terms[(i, j)], lazy[(i, j)] = t, lz
         downs = [(i, j) for i, _ in rows for j in range(nb) if j < i]
         cur = {(i, j): xs[j] for i, j in downs}
         for k in range(max((i - j for i, j in downs), default=0)):
             live = [(i, j) for i, j in downs if k < i - j]
+            lz_dn = [ops.LazyBN() if ops.FUSE_LAZY and k == i - j - 1 else None for i, j in live]
             outs = _run_convbn_seqs([self.fuse_layers[i][j][k] for i, j in live],
                                     [cur[ij] for ij in live],
-                                    [links[j] if k == 0 else None for _, j in live])
+                                    [links[j] if k == 0 else None for _, j in live], lz_dn)
             cur.update(zip(live, outs))
+            lazy.update((ij, lz) for ij, lz in zip(live, lz_dn) if lz is not None or
+                        k == ij[0] - ij[1] - 1)
         terms.update(cur)
         out = []
         for i, _ in rows:
             out.append(ops.fuse_sum_relu([xs[j] if j == i else terms[(i, j)] for j in range(nb)],
                                          xs[i].shape[1:3],
-                                         [links[i] if j == i else None for j in range(nb)]))
+                                         [links[i] if j == i else None for j in range(nb)],
+                                         [None if j == i else lazy.get((i, j)) for j in range(nb)]))
         return out
 
 

@@ -168,6 +168,7 @@ class ResBN:
 
 RES_BN = True  # False: the shortcut BN output is stored (A/B and parity tests)
 MASK_BYTES = True  # residual layers keep their ReLU mask as bytes for the backward (vs y)
+FUSE_LAZY = True   # fuse units' BN outputs formed inside the fuse sum, never stored (A/B)
 
 
 def lazy_bn_ok(shape, conv):
@@ -1112,7 +1113,7 @@ def _up_bwd_pow2(g, shapes):
 
 class _FuseSum(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, out_hw, links, *terms):
+    def forward(ctx, out_hw, links, lazies, *terms):
         ref = terms[0]
         n, c = ref.shape[0], ref.shape[3]
         y = new_act((n, out_hw[0], out_hw[1], c), ref)
@@ -1123,7 +1124,15 @@ class _FuseSum(torch.autograd.Function):
             ptrs[i] = p_
             acts[i] = a_
         yp, ya = act_of(y)
-        call("vae2_fuse_sum_relu", len(terms), ptrs, acts, yp, ctypes.byref(ya), stream_ptr())
+        if lazies is not None and any(lz is not None for lz in lazies):
+            # terms that are a fuse unit's pre-BN output, normalised here (never stored)
+            sv = (ctypes.c_void_p * len(terms))(*[ptr(lz.save) if lz is not None else None
+                                                  for lz in lazies])
+            call("vae2_fuse_sum_relu_bn", len(terms), ptrs, acts, sv, yp, ctypes.byref(ya),
+                 stream_ptr())
+        else:
+            call("vae2_fuse_sum_relu", len(terms), ptrs, acts, yp, ctypes.byref(ya),
+                 stream_ptr())
         ctx.shapes = [tuple(t.shape) for t in terms]
         ctx.links = links
         ctx.save_for_backward(y)
@@ -1139,7 +1148,7 @@ class _FuseSum(torch.autograd.Function):
         gp, ga = act_of(g)
         links = ctx.links or (None,) * len(ctx.shapes)
         lk = next((i for i, l in enumerate(links) if l is not None), None)
-        if lk is not None and ctx.needs_input_grad[lk + 2]:
+        if lk is not None and ctx.needs_input_grad[lk + 3]:
             # the identity term's input has other consumers (ops.GradLink): its share of
             # the gradient goes straight into (or onto) their shared buffer
             link = links[lk]
@@ -1157,10 +1166,10 @@ class _FuseSum(torch.autograd.Function):
                  ctypes.byref(ga), stream_ptr())
         grads = []
         ups = [i for i, shp in enumerate(ctx.shapes)
-               if ctx.needs_input_grad[i + 2] and i != lk and shp[1:3] != tuple(y.shape[1:3])]
+               if ctx.needs_input_grad[i + 3] and i != lk and shp[1:3] != tuple(y.shape[1:3])]
         upg = _up_bwd_pow2(g, [ctx.shapes[i] for i in ups]) if ups else None
         for i, shp in enumerate(ctx.shapes):
-            if not ctx.needs_input_grad[i + 2]:
+            if not ctx.needs_input_grad[i + 3]:
                 grads.append(None)
             elif i == lk:
                 grads.append(links[i].finish())
@@ -1170,13 +1179,17 @@ class _FuseSum(torch.autograd.Function):
                 grads.append(upg[ups.index(i)])
             else:
                 grads.append(_up_bwd(g, shp))
-        return (None, None, *grads)
+        return (None, None, None, *grads)
 
 
-def fuse_sum_relu(terms, out_hw, links=None):
+def fuse_sum_relu(terms, out_hw, links=None, lazies=None):
     """relu(sum of terms), lower-resolution terms bilinearly upsampled to out_hw.  links:
-    per term an ops.GradLink (or None) shared with the term's other consumers."""
-    return _FuseSum.apply(tuple(out_hw), tuple(links) if links else None, *terms)
+    per term an ops.GradLink (or None) shared with the term's other consumers.  lazies:
+    per term a LazyBN (or None): the term is that BatchNorm layer's pre-BN output, its
+    normalised output (the fuse unit's BN, no ReLU) is formed here and never stored; the
+    gradient returned for the term is the one of that normalised output (LazyBN's rule)."""
+    return _FuseSum.apply(tuple(out_hw), tuple(links) if links else None,
+                          tuple(lazies) if lazies else None, *terms)
 
 
 class _UpCat(torch.autograd.Function):
