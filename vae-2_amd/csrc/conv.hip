@@ -1178,9 +1178,10 @@ int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persisten
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
 int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
 int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
+int g_wgrad_cols = 0;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide, g_igemm_minblk;
+    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1959,6 +1960,12 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   t.tm = mt <= 4 ? mt : 4;
   t.gy = (int)ceil_div(cout, 16 * t.tm);
   int ct = (ncol4 + 15) / 16;
+  // tune key 1: when 4 row tiles would leave a third-empty second column block (ct = 4:
+  // 64 columns as 48 + 48), take 2 row tiles and all 64 columns in one block instead
+  if (g_wgrad_cols && t.tm == 4 && ct == 4) {
+    t.tm = 2;
+    t.gy = (int)ceil_div(cout, 32);
+  }
   const int tn_max = t.tm == 4 ? 3 : 4;  // <4,4> would not fit 2 waves/SIMD without spills
   t.tn = ct <= tn_max ? ct : tn_max;
   t.gx = (int)ceil_div(ncol4, 16 * t.tn);
@@ -2401,6 +2408,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 0) {
     const int prev = g_igemm_minblk;
     g_igemm_minblk = value < 0 ? 0 : value;
+    return prev;
+  }
+  if (key == 1) {
+    const int prev = g_wgrad_cols;
+    g_wgrad_cols = value ? 1 : 0;
     return prev;
   }
   return -1;
