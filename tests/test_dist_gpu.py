@@ -183,12 +183,16 @@ def _w18_work(rank, world, port, q):
     loss = losses[0].detach().clone()
     orig(loss)
     gsum = float(torch.cat([f.grad for f in opt.flats]).double().sum())
-    out = [float(loss) / world, x2p.detach().cpu(), x3p.detach().cpu(), gsum, exchanges]
+    # numpy by value: torch's queue would share tensors through a socket of this process,
+    # which may be gone when the parent unpickles them
+    out = [float(loss) / world, x2p.detach().cpu().numpy(), x3p.detach().cpu().numpy(), gsum,
+           exchanges]
     if rank == 0:  # the averaged gradients (identical on both ranks: gsum) per parameter
         from test_model_gpu import named_params
-        out.append({n: p.main_grad.detach().cpu().clone() for n, p in
+        out.append({n: p.main_grad.detach().cpu().numpy().copy() for n, p in
                     named_params(("encz", fm.encz_model), ("ed", fm.encdec_model))})
     q.put((rank, "ok", *out))
+    dist.barrier()  # both results sent before either process exits
     dist.destroy_process_group()
 
 
@@ -244,13 +248,13 @@ def test_two_ranks_w18_sync_bn_matches_oracle():
     loss = res[0][2]
     assert abs(res[1][2] - loss) <= 1e-7 * abs(loss)  # the reduced loss on both ranks
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
-    x2 = torch.cat([res[0][3], res[1][3]])
-    x3 = torch.cat([res[0][4], res[1][4]])
+    x2 = torch.from_numpy(np.concatenate([res[0][3], res[1][3]]))
+    x3 = torch.from_numpy(np.concatenate([res[0][4], res[1][4]]))
     assert max_rel(x2, preds[1]) < 1e-4, max_rel(x2, preds[1])
     assert max_rel(x3, preds[2]) < 1e-3, max_rel(x3, preds[2])
     assert res[0][5] == res[1][5]  # identical averaged gradients on both ranks
     assert res[0][6] < 600, res[0][6]  # SyncBN exchanges per step, batched per depth level
-    grads = res[0][7]
+    grads = {n: torch.from_numpy(g) for n, g in res[0][7].items()}
 
     class _P:
         def __init__(self, g):

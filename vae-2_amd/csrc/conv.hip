@@ -717,17 +717,20 @@ constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 8;
 // BNX (compile time, so the plain instances carry none of it): 1 = input BatchNorm in the
 // staging (DConv::isave, forward), 2 = producer BatchNorm backward partials in the
 // epilogue (DConv::bx, data gradient).
-template <int TM, int TN, bool FLIP, bool BF, int NR = 0, int BNX = 0>
+// NW = waves per workgroup (4, or 8 with TM = 2: the same 8-row tile as TM = 4, each wave
+// owning one row -- twice the waves per SIMD for the same LDS tile)
+template <int TM, int TN, bool FLIP, bool BF, int NR = 0, int BNX = 0, int NW = 4>
 __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const int by,
                                             const int nrows, float* __restrict__ tile) {
-  constexpr int BH = 2 * TM, LH = BH + 2, LW = kDcBW + 2;
+  constexpr int NT = 64 * NW;
+  constexpr int BH = NW * TM / 2, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
   constexpr int BNT = BN + NR;             // channels of this block (MFMA + VALU)
   constexpr int PPW = 16 * TM;             // output pixels per wave
   constexpr int LPP = NR ? 64 / PPW : 1;   // lanes per pixel (remainder channel groups)
   constexpr int NRL = NR / LPP;            // remainder channels per lane
   static_assert(NR == 0 || (!BF && NR % LPP == 0 && NRL >= 1 && NRL <= 8), "remainder shape");
-  __shared__ float red[4][2][BNT];
+  __shared__ float red[NW][2][BNT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int per_img = p.tiles_h * p.tiles_w;
@@ -801,7 +804,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     }
     if constexpr (NR > 0) {  // remainder weights of the slab [j][(tap, quad)][4], FLIP
       const int per = ((9 * qs + 7) >> 3) * 32;  // whole chunk pairs: zero tail
-      for (int i = threadIdx.x; i < NR * per; i += 256) {
+      for (int i = threadIdx.x; i < NR * per; i += NT) {
         const int j = i / per, rem = i - j * per;
         const int t = rem / (qs * 4), c = rem - t * (qs * 4);
         const int tl = FLIP ? 8 - t : t;
@@ -813,7 +816,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     // flight per thread before their LDS stores (few round trips, few extra registers)
     constexpr int SB = 3;
     {
-    const int sq = threadIdx.x % qs, pb = threadIdx.x / qs, pstride = 256 / qs;
+    const int sq = threadIdx.x % qs, pb = threadIdx.x / qs, pstride = NT / qs;
     const int c = (q0 + sq) * 4;
     const bool cpad = c + 4 > p.a_c;
     // input BatchNorm (FLIP = false only): this thread's channel quad's scale / shift
@@ -1112,22 +1115,26 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     }
     __syncthreads();
     const int rows = nrows;
-    for (int c = threadIdx.x; c < BNT; c += 256) {
+    for (int c = threadIdx.x; c < BNT; c += NT) {
       if (n0 + c >= p.n) continue;
-      float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-      float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+      float s = red[0][0][c], s2 = red[0][1][c];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        s += red[w][0][c];
+        s2 += red[w][1][c];
+      }
       p.stats[bm * p.n + n0 + c] = s;
       p.stats[(rows + bm) * p.n + n0 + c] = s2;
     }
   }
 }
 
-template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0, int BNX = 0>
-__global__ __launch_bounds__(256) void dconv3_kernel(DConv p) {
+template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0, int BNX = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void dconv3_kernel(DConv p) {
   static_assert(BNX == 0 || (!BF && (BNX == 1) != FLIP), "input BN: forward; partials: dgrad");
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  dconv3_body<TM, TN, FLIP, BF, NR, BNX>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.x,
-                                    tile);
+  dconv3_body<TM, TN, FLIP, BF, NR, BNX, NW>(p, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y,
+                                             gridDim.x, tile);
 }
 
 // Up to kDcGroup independent layers with the same tile shape in one launch (the lock-
@@ -1179,9 +1186,10 @@ int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-tran
 int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
 int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
 int g_wgrad_cols = 0;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
+int g_dconv_nw8 = 0;      // vae2_conv2d_set_tune key 2: direct 3x3 8-row tiles as 8 waves
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols;
+    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2066,6 +2074,7 @@ using namespace vae2;
 struct DTile {
   int tm, tn, nblk, cs4, tiles_h, tiles_w;
   int nr = 0;  // output channels on the VALU beside the MFMA tiles (dconv3_body NR)
+  int nw = 4;  // waves per workgroup (dconv3_body NW); tile rows = nw * tm / 2
 };
 
 
@@ -2104,7 +2113,13 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   // (from the all-MFMA N blocking, so the tile rows and the BN partial-statistics rows
   //  do not depend on the remainder switch or the grouped path)
   if (yd->h < 8 || ad->n * ceil_div(yd->h, 8) * d.tiles_w * t.nblk < 768) d.tm = 2;
-  d.tiles_h = (int)ceil_div(yd->h, 2 * d.tm);
+  // tune key 2: the 8-row tiles as 8 waves of one row each (TM = 2, NW = 8) -- same tile
+  // rows, so the same BN partial-statistics rows
+  if (g_dconv_nw8 && d.tm == 4 && !g_bf16) {
+    d.tm = 2;
+    d.nw = 8;
+  }
+  d.tiles_h = (int)ceil_div(yd->h, d.nw * d.tm / 2);
   // the remainder form has one N block: only where the tiles alone fill the chip twice
   // (algo 2 forces it wherever legal, for the tests)
   if (d.nr && g_conv_algo != 2 && ad->n * d.tiles_h * d.tiles_w < 512) {
@@ -2139,36 +2154,36 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
                  const BnSide& bn = BnSide{});
 
 #if VAE2_PART(2)
-template <int TM, bool FLIP>
+template <int TM, bool FLIP, int NW = 4>
 static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s,
                             int nr = 0) {
   if (p.isave || p.bx) {  // fused BatchNorm (fp32 operands): forward input / dgrad partials
     constexpr int X = FLIP ? 2 : 1;
     if (nr) {
-      if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2, X>), grid, dim3(256), shm, s, p);
-      else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4, X>), grid, dim3(256), shm, s, p);
-      else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8, X>), grid, dim3(256), shm, s, p);
+      if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2, X, NW>), grid, dim3(64 * NW), shm, s, p);
+      else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4, X, NW>), grid, dim3(64 * NW), shm, s, p);
+      else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8, X, NW>), grid, dim3(64 * NW), shm, s, p);
       return;
     }
     switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, false, 0, X>), grid, dim3(256), shm, s, p); break;
+  case T: VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, false, 0, X, NW>), grid, dim3(64 * NW), shm, s, p); break;
       CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
     }
     return;
   }
   if (nr) {  // fp32 operands (pick_dtile)
-    if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2>), grid, dim3(256), shm, s, p);
-    else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4>), grid, dim3(256), shm, s, p);
-    else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8>), grid, dim3(256), shm, s, p);
+    if (tn == 1 && nr == 2) VAE2_LAUNCH((dconv3_kernel<TM, 1, FLIP, false, 2, 0, NW>), grid, dim3(64 * NW), shm, s, p);
+    else if (tn == 2 && nr == 4) VAE2_LAUNCH((dconv3_kernel<TM, 2, FLIP, false, 4, 0, NW>), grid, dim3(64 * NW), shm, s, p);
+    else VAE2_LAUNCH((dconv3_kernel<TM, 4, FLIP, false, 8, 0, NW>), grid, dim3(64 * NW), shm, s, p);
     return;
   }
   switch (tn) {
 #define CASE(T) \
   case T:                                                                         \
-    if (g_bf16) VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, true>), grid, dim3(256), shm, s, p); \
-    else VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP>), grid, dim3(256), shm, s, p);        \
+    if (g_bf16) VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, true, 0, 0, NW>), grid, dim3(64 * NW), shm, s, p); \
+    else VAE2_LAUNCH((dconv3_kernel<TM, T, FLIP, false, 0, 0, NW>), grid, dim3(64 * NW), shm, s, p);        \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
@@ -2192,7 +2207,7 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
 }
 
 static size_t dconv_shm(const DTile& d) {
-  return ((size_t)(2 * d.tm + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) +
+  return ((size_t)(d.nw * d.tm / 2 + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) +
           (size_t)d.nr * ((9 * d.cs4 + 7) / 8) * 32 + 2 * kDcTab) * sizeof(float);
 }
 
@@ -2227,7 +2242,10 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.vec_out = g_vec_out && vec_ok(y, (int)yd->ps) && !(stats && beta != 0.f);
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
   const size_t shm = dconv_shm(d);
-  if (d.tm == 4) {
+  if (d.nw == 8) {
+    if (flip) dconv_launch_tn<2, true, 8>(p, d.tn, grid, shm, s, d.nr);
+    else dconv_launch_tn<2, false, 8>(p, d.tn, grid, shm, s, d.nr);
+  } else if (d.tm == 4) {
     if (flip) dconv_launch_tn<4, true>(p, d.tn, grid, shm, s, d.nr);
     else dconv_launch_tn<4, false>(p, d.tn, grid, shm, s, d.nr);
   } else {
@@ -2413,6 +2431,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 1) {
     const int prev = g_wgrad_cols;
     g_wgrad_cols = value ? 1 : 0;
+    return prev;
+  }
+  if (key == 2) {
+    const int prev = g_dconv_nw8;
+    g_dconv_nw8 = value ? 1 : 0;
     return prev;
   }
   return -1;
@@ -2743,7 +2766,8 @@ int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
                   (fwd ? conv_shapes_ok(ad, od, J.k, J.stride, J.pad)
                        : conv_shapes_ok(od, ad, J.k, J.stride, J.pad)) &&
                   fits32(ad) && fits32(od) && dconv_use(ad, od, J.k, J.stride, J.pad, J.x) &&
-                  pick_dtile(ad, od).nr == 0;  // (remainder layers: their own launch)
+                  pick_dtile(ad, od).nr == 0 &&  // (remainder layers: their own launch)
+                  pick_dtile(ad, od).nw == 4;    // (8-wave tiles: their own launch)
     if (!direct) {
       int rc = fwd ? vae2_conv2d_fwd(J.x, ad, J.wp, J.bias, J.y, od, J.k, J.stride, J.pad,
                                      J.beta, J.stats, stream)
