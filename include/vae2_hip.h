@@ -75,8 +75,9 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * reaches it; 0 = the default rule); key 1 = 1: weight gradients with 64 (tap, Cin4)
  * columns take 2 x 16 output-channel rows and all 64 columns per workgroup (not 4 x 16
  * rows and 48 + 48 columns); key 2 = 1: the direct 3x3 kernels' 8-row tiles run as 8
- * waves of one row each (512 threads) instead of 4 waves of two rows.  Returns the
- * previous value, -1 for an unknown key.                                                */
+ * waves of one row each (512 threads) instead of 4 waves of two rows; key 3 = 1: the
+ * 18 / 36 / 72-channel 3x3 weight gradients spread their column tiles over 8 waves.
+ * Returns the previous value, -1 for an unknown key.                                    */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
@@ -87,6 +88,10 @@ int vae2_conv2d_set_tune(int key, int value);
  * until the flush is enqueued.  Returns the previous setting.                        */
 int vae2_wgrad_defer(int on);
 int vae2_wgrad_flush(void* stream);
+/* ABI 10: launch only the queued reductions that were queued from `stream`, on it (no
+ * cross-stream ordering needed: a sub-network on a side stream -- the posterior net --
+ * finishes its own weight gradients while other streams' stay queued).              */
+int vae2_wgrad_flush_stream(void* stream);
 
 /* Independent convolutions in one call (the lock-stepped layers of one HRNet depth
  * level).  Each job is one vae2_conv2d_fwd (kind 0: x, xd -> y, yd with bias, beta,

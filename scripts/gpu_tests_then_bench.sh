@@ -6,10 +6,10 @@ TAG=${1:-tb}; K=${2:-}; shift 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -n "$K" ]; then
-  timeout -k 10 900 python -u -m pytest -x -v --timeout 420 --timeout-method thread tests -m gpu \
+  timeout -k 10 900 python -u -m pytest --maxfail=4 -v --timeout 420 --timeout-method thread tests -m gpu \
     -k "$K" > gpurun_out/${TAG}_tests.log 2>&1
 else
-  timeout -k 10 900 python -u -m pytest -x -v --timeout 420 --timeout-method thread tests -m gpu \
+  timeout -k 10 900 python -u -m pytest --maxfail=4 -v --timeout 420 --timeout-method thread tests -m gpu \
     > gpurun_out/${TAG}_tests.log 2>&1
 fi
 rc=$?; tail -3 gpurun_out/${TAG}_tests.log

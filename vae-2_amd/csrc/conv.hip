@@ -1187,9 +1187,10 @@ int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 
 int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
 int g_wgrad_cols = 0;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
 int g_dconv_nw8 = 0;      // vae2_conv2d_set_tune key 2: direct 3x3 8-row tiles as 8 waves
+int g_wgrad_nw8 = 0;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients over 8 waves
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8;
+    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1590,8 +1591,11 @@ struct WGrad3 {
 // the 4 lane groups' sums are combined at the end.  The MFMA work of an 18-channel
 // layer halves (32 -> 16 rows), of a 36-channel one drops by 1/3.  With several co slabs
 // (72 = 2 x (32 + 4)) each slab is 16*TM + NR channels wide.
-template <int TM, int TN, int BH, bool PF, int KS, bool BF = false, int NR = 0>
-__global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
+// NW = waves per workgroup: 4, or 8 (each wave half the column tiles: twice the waves per
+// SIMD for layers whose grid leaves one workgroup per CU)
+template <int TM, int TN, int BH, bool PF, int KS, bool BF = false, int NR = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void wgrad3_kernel(WGrad3 p) {
+  constexpr int NT = 64 * NW;
   constexpr int HALO = KS / 2, TAPS = KS * KS;
   constexpr int LH = BH + KS - 1, LW = 32 + KS - 1, NPX = BH * 32, LPX = LH * LW;
   constexpr int QMAX = KS == 1 ? 16 : 9;  // channel quads per slab
@@ -1619,7 +1623,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     const bool ok = t < TAPS && cl < csw_real;
     bbase[j] = ok ? cl * LPX + (t / KS) * LW + (t % KS) : p.csw * LPX;
   }
-  for (int i = threadIdx.x; i < LPX; i += 256) xt[p.csw * LPX + i] = 0.f;
+  for (int i = threadIdx.x; i < LPX; i += NT) xt[p.csw * LPX + i] = 0.f;
   // input BatchNorm: the slab's scale / shift (read after the tile loop's first barrier)
   __shared__ float ibn[2][QMAX * 4];
   if (p.isave && threadIdx.x < QMAX * 4) {
@@ -1651,8 +1655,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   const int te = tb + p.tiles_per_split < p.ntiles ? tb + p.tiles_per_split : p.ntiles;
   // Register prefetch: tile t+1's global loads are in flight while tile t computes.
   constexpr int NDY = NPX * NQ;                 // dY items (f4 = 4 co of one pixel)
-  constexpr int NI = (NDY + 255) / 256;         // dY items per thread
-  constexpr int NX = (LPX * QMAX + 255) / 256;  // X items per thread
+  constexpr int NI = (NDY + NT - 1) / NT;         // dY items per thread
+  constexpr int NX = (LPX * QMAX + NT - 1) / NT;  // X items per thread
   const int xtotal = LPX * (csw_real >> 2);
   f4 pdy[NI], pxx[NX];
   static_assert(NX <= 32, "x item mask");
@@ -1665,7 +1669,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     const int ibase = img * p.h;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-      const int i = threadIdx.x + u * 256;
+      const int i = threadIdx.x + u * NT;
       const int q = i / NPX, px = i - q * NPX;
       const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
       const int co = co0 + 4 * q;
@@ -1674,7 +1678,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
-      const int i = threadIdx.x + u * 256;
+      const int i = threadIdx.x + u * NT;
       const int q = i / LPX, hp = i - q * LPX;
       const int lr = hp / LW, lc = hp - lr * LW;
       const int ih = oh0 - HALO + lr, iw = ow0 - HALO + lc;
@@ -1687,8 +1691,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
   auto store = [&]() {
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-      const int i = threadIdx.x + u * 256;
-      if (NDY % 256 != 0 && i >= NDY) break;
+      const int i = threadIdx.x + u * NT;
+      if (NDY % NT != 0 && i >= NDY) break;
       const int q = i / NPX, px = i - q * NPX;
       const int co = co0 + 4 * q;
 #pragma unroll
@@ -1696,7 +1700,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
     }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
-      const int i = threadIdx.x + u * 256;
+      const int i = threadIdx.x + u * NT;
       if (i < xtotal) {
         const int q = i / LPX, hp = i - q * LPX;
         const int c = c0 + 4 * q;
@@ -1721,7 +1725,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
         f4 v[NI];
 #pragma unroll
         for (int u = 0; u < NI; ++u) {
-          const int i = threadIdx.x + u * 256;
+          const int i = threadIdx.x + u * NT;
           const int q = i / NPX, px = i - q * NPX;
           const int oh = oh0 + px / 32, ow = ow0 + (px & 31);
           const int co = co0 + 4 * q;
@@ -1730,8 +1734,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
         }
 #pragma unroll
         for (int u = 0; u < NI; ++u) {
-          const int i = threadIdx.x + u * 256;
-          if (NDY % 256 != 0 && i >= NDY) break;
+          const int i = threadIdx.x + u * NT;
+          if (NDY % NT != 0 && i >= NDY) break;
           const int q = i / NPX, px = i - q * NPX;
           const int co = co0 + 4 * q;
 #pragma unroll
@@ -1739,12 +1743,12 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
             dyt[(4 * q + k) * DYS + px] = co + k < p.cout ? v[u][k] : 0.f;
         }
       }
-      for (int i0 = threadIdx.x; i0 < xtotal; i0 += 4 * 256) {
+      for (int i0 = threadIdx.x; i0 < xtotal; i0 += 4 * NT) {
         f4 v[4];
         bool okv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int i = i0 + u * 256;
+          const int i = i0 + u * NT;
           const int q = i / LPX, hp = i - q * LPX;
           const int lr = hp / LW, lc = hp - lr * LW;
           const int ih = oh0 - HALO + lr, iw = ow0 - HALO + lc;
@@ -1756,7 +1760,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3 p) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int i = i0 + u * 256;
+          const int i = i0 + u * NT;
           if (i >= xtotal) break;
           const int q = i / LPX, hp = i - q * LPX;
           const int c = c0 + 4 * q;
@@ -2267,6 +2271,7 @@ struct W3Tile {
   int ks, tm, tn, bh, csw, n_ci_slabs, n_co_slabs, tiles_h, tiles_w, ntiles, tps, splits;
   bool pf;
   int nr = 0;  // output channels on the VALU beside the MFMA rows (wgrad3_kernel NR)
+  int nw = 4;  // waves per workgroup (wgrad3_kernel NW)
 };
 
 static bool wgrad3_shape_ok(const vae2_act* xd, const vae2_act* dyd, int k, int stride, int pad) {
@@ -2295,6 +2300,14 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
     t.tm = dyd->c == 18 ? 1 : 2;
     t.nr = dyd->c == 18 ? 2 : 4;
     t.n_co_slabs = (int)(dyd->c / (16 * t.tm + t.nr));
+  }
+  // tune key 3: the remainder layers' column tiles over 8 waves (twice the waves per SIMD)
+  if (g_wgrad_nw8 && t.nr && !g_bf16) {
+    const int tn2 = (nt + 7) / 8;
+    if ((t.tm == 1 && tn2 == 2) || (t.tm == 2 && tn2 == 3)) {
+      t.tn = tn2;
+      t.nw = 8;
+    }
   }
   t.bh = (t.tm <= 2 && t.csw <= 24 && k == 3) ? 8 : 4;
   t.tiles_h = (int)ceil_div(dyd->h, t.bh);
@@ -2337,8 +2350,13 @@ static size_t wgrad3_lds(const W3Tile& t) {
 #if VAE2_PART(3)
 template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
-                             hipStream_t s, int nr = 0) {
+                             hipStream_t s, int nr = 0, int nw = 4) {
   if constexpr (TM == 1 || TM == 2) {
+    if (nr && nw == 8) {  // 8 waves: (TM, TN) = (1, 2) or (2, 3) (pick_w3tile)
+      constexpr int R = TM == 1 ? 2 : 4, T8 = TM == 1 ? 2 : 3;
+      VAE2_LAUNCH((wgrad3_kernel<TM, T8, BH, PF, 3, false, R, 8>), grid, dim3(512), shm, s, p);
+      return;
+    }
     if (nr) {  // (TM, NR) = (1, 2) or (2, 4): pick_w3tile, fp32 operands
       constexpr int R = TM == 1 ? 2 : 4;
       switch (tn) {
@@ -2370,8 +2388,8 @@ template <int BH, bool PF>
 static void wgrad3_launch_tm(const WGrad3& p, const W3Tile& t, dim3 grid, size_t shm,
                              hipStream_t s) {
   switch (t.tm) {
-    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr); break;
-    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr); break;
+    case 1: wgrad3_launch_tn<1, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr, t.nw); break;
+    case 2: wgrad3_launch_tn<2, BH, PF>(p, t.tn, t.ks, grid, shm, s, t.nr, t.nw); break;
     case 3: wgrad3_launch_tn<3, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
     default: wgrad3_launch_tn<4, BH, PF>(p, t.tn, t.ks, grid, shm, s); break;
   }
@@ -2438,6 +2456,11 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_dconv_nw8 = value ? 1 : 0;
     return prev;
   }
+  if (key == 3) {
+    const int prev = g_wgrad_nw8;
+    g_wgrad_nw8 = value ? 1 : 0;
+    return prev;
+  }
   return -1;
 }
 
@@ -2456,13 +2479,19 @@ int vae2_wgrad_defer(int on) {
   return prev;
 }
 
-int vae2_wgrad_flush(void* stream) {
+static int wgrad_flush_impl(void* stream, bool own_only) {
   const char* fn = "vae2_wgrad_flush";
   hipStream_t want = as_stream(stream);
   std::vector<WRQueued> q;
   {
     std::lock_guard<std::mutex> lk(g_wr_mu);
-    q.swap(g_wr_queue);
+    if (own_only) {  // only the jobs queued from this stream (no cross-stream ordering)
+      std::vector<WRQueued> keep;
+      for (const WRQueued& j : g_wr_queue) (j.stream == want ? q : keep).push_back(j);
+      g_wr_queue.swap(keep);
+    } else {
+      q.swap(g_wr_queue);
+    }
   }
   size_t i = 0;
   // every job on the given stream: the caller orders it after the jobs' own streams
@@ -2495,6 +2524,12 @@ int vae2_wgrad_flush(void* stream) {
   }
   return 0;
 }
+
+int vae2_wgrad_flush(void* stream) { return wgrad_flush_impl(stream, false); }
+
+int vae2_wgrad_flush_stream(void* stream) { return wgrad_flush_impl(stream, true); }
+
+
 
 #endif  // VAE2_PART(3)
 

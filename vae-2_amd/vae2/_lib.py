@@ -62,6 +62,7 @@ _SIGS = {
     "vae2_conv2d_set_tune": (c_int, [c_int, c_int]),
     "vae2_wgrad_defer": (c_int, [c_int]),
     "vae2_wgrad_flush": (c_int, [c_vp]),
+    "vae2_wgrad_flush_stream": (c_int, [c_vp]),
     "vae2_conv2d_set_algo": (c_int, [c_int]),
     "vae2_conv2d_fwd": (c_int, [c_vp, P_ACT, c_vp, c_vp, c_vp, P_ACT, c_int, c_int, c_int,
                                 c_f32, c_vp, c_vp]),

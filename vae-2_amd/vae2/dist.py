@@ -111,11 +111,18 @@ def tail_range(flat, prefixes=("decf_", "decp_")):
     return flat.offsets[idx[0]]
 
 
-def _start_range(flat, lo, hi):
+def _start_range(flat, lo, hi, own_stream=False):
     """Flush the queued weight-gradient reductions, join the side streams, then start the
-    bucketed all-reduce of flat.grad[lo:hi] (recorded in _EARLY for allreduce_grads)."""
-    ops.flush_wgrad()   # queued weight-gradient reductions (they write the range)
-    streams.join_all()  # side-stream work (the posterior net, the past decoder)
+    bucketed all-reduce of flat.grad[lo:hi] (recorded in _EARLY for allreduce_grads).
+    own_stream: the range is written only by work issued on the current stream (a
+    sub-network on its own side stream): flush that stream's reductions, no join -- a
+    join would not order this stream after a HIP graph's capture stream, whose queued
+    reductions a full flush would launch here."""
+    if own_stream:
+        ops.flush_wgrad(own_stream=True)
+    else:
+        ops.flush_wgrad()   # queued weight-gradient reductions (they write the range)
+        streams.join_all()  # side-stream work (the posterior net, the past decoder)
     buf = flat.grad
     if EARLY_CHECK is not None:  # the range as the buckets see it (no later write allowed)
         EARLY_CHECK.append((buf, lo, hi, buf[lo:hi].clone()))
@@ -154,7 +161,7 @@ class _Anchor(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, *_):
         flat, lo, hi = ctx.args
-        _start_range(flat, lo, hi)
+        _start_range(flat, lo, hi, own_stream=True)  # the network ran on this stream
         return gx, None, None, None, None
 
 

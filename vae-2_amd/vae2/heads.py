@@ -243,7 +243,7 @@ class _Heads(torch.autograd.Function):
                                  ctypes.byref(ga), ctypes.c_void_p(wsink.data_ptr() + 4 * c0),
                                  C, None, 1, 1, 0, 1, ptr(ws2), wsz2, s)
                         if wret is None:
-                            _WS_HOLD.append(ws2)
+                            _WS_HOLD.append((torch.cuda.current_stream().cuda_stream, ws2))
                     if ctx.needs_input_grad[2 + j]:
                         first = dxs[j] is None
                         if first:

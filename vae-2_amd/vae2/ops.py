@@ -416,21 +416,29 @@ def _conv_fwd_queued(group, x, weight, bias, spec, stats):
 
 
 _WGRAD_BATCH = [0]  # open wgrad_batch contexts
-_WS_HOLD = []       # workspaces of queued weight-gradient reductions
+_WS_HOLD = []       # (queueing stream handle, workspace) of queued weight-gradient reductions
 _WGRAD_CB = [False, -1]  # end-of-backward flush queued with the engine, by graph task id
 
 
-def flush_wgrad():
+def flush_wgrad(own_stream=False):
     """Launch every queued weight-gradient reduction on the current stream, after the
     side streams' work (the convs that wrote the partial slabs), and release the held
-    workspaces (recorded on this stream, so the allocator reuses them only after it)."""
-    streams.join_all()
+    workspaces (recorded on this stream, so the allocator reuses them only after it).
+    own_stream: only the reductions queued from the current stream (their slabs were
+    written on it: no join), the others stay queued with their workspaces held."""
     cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+    if own_stream:
+        key = cur.cuda_stream if cur is not None else None
+        call("vae2_wgrad_flush_stream", stream_ptr())
+        keep = [(k, t_) for k, t_ in _WS_HOLD if k != key]
+        _WS_HOLD[:] = keep
+        return
+    streams.join_all()
     try:
         call("vae2_wgrad_flush", stream_ptr())
     finally:
         if cur is not None:
-            for t_ in _WS_HOLD:
+            for _, t_ in _WS_HOLD:
                 if t_.is_cuda:
                     t_.record_stream(cur)
         _WS_HOLD.clear()
@@ -527,8 +535,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
             else:
                 call("vae2_conv2d_bwd_weight", xp, ctypes.byref(xa), dyp, ctypes.byref(dya),
                      ptr(wsink), ptr(bsink), spec.k, spec.stride, spec.pad, 1, ptr(ws), size, s)
-        if _WGRAD_BATCH[0] and not now:
-            _WS_HOLD.append(ws)  # the deferred reduction reads it at the flush
+        if _WGRAD_BATCH[0] and not now:  # the deferred reduction reads it at the flush
+            _WS_HOLD.append((torch.cuda.current_stream().cuda_stream, ws))
     dx = None
     if need_dx:
         link = spec.x_link
