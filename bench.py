@@ -94,9 +94,8 @@ def parse():
                          "GAN_LAMBDA 1 (both LSGAN generator terms through the two "
                          "discriminators) + the discriminator step with its own Adam")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="replay the step as one captured HIP graph, RCCL collectives "
-                         "included at N > 1 (auto = on; tests/test_dist_rccl_gpu.py holds "
-                         "the captured distributed step bit-identical to eager steps).  The "
+                    help="replay the step as one captured HIP graph (auto: at N=1; the "
+                         "distributed step under capture is not enabled, DESIGN.md (e)).  The "
                          "eager step measured 0-3%% faster on an idle host but 10-20%% "
                          "slower when the host CPUs are busy; the graph replay is stable")
     return ap.parse_args()
@@ -301,7 +300,7 @@ def main():
             opt_d.step()
         return losses[0]
 
-    use_graph = args.graph in ("on", "auto")
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
     step = eager_step
     if use_graph:
         from vae2.graph import StepGraph
