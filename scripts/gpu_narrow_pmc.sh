@@ -15,7 +15,7 @@ for i in $IDX; do
   p=0
   for grp in "$G1" "$G2" "$G3"; do
     p=$((p+1))
-    timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "dconv3|wgrad3|igemm|wgrad_kernel" \
+    timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "dconv3|wgrad3|igemm|wgrad_kernel|gemm1x1" \
       -f csv -d gpurun_out/${TAG}_s${i}_p$p -o run -- python vae-2_amd/tools/conv_bench.py \
       --only $i --iters 5 > gpurun_out/${TAG}_s${i}_p$p.log 2>&1
     rc=$?; echo "shape $i pass $p rc=$rc"

@@ -11,5 +11,5 @@ for tune in "" "0=512" "0=1024" "1=1" "2=1" "3=1"; do
     > gpurun_out/${TAG}_cb_${tune:-default}.log 2>&1 || { tail -5 gpurun_out/${TAG}_cb_${tune:-default}.log; exit 1; }
   echo "== tune '${tune}'"; grep "weighted" gpurun_out/${TAG}_cb_${tune:-default}.log
 done
-bash scripts/gpu_narrow_pmc.sh ${TAG}_n "3 4 5 9" || exit 1
+bash scripts/gpu_narrow_pmc.sh ${TAG}_n "2 3 4 5 9" || exit 1
 bash scripts/gpu_bench_prof.sh ${TAG} || exit 1
