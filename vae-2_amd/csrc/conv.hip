@@ -726,10 +726,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   constexpr int BH = NW * TM / 2, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
   constexpr int BNT = BN + NR;             // channels of this block (MFMA + VALU)
-  constexpr int PPW = 16 * TM;             // output pixels per wave
-  constexpr int LPP = NR ? 64 / PPW : 1;   // lanes per pixel (remainder channel groups)
-  constexpr int NRL = NR / LPP;            // remainder channels per lane
-  static_assert(NR == 0 || (!BF && NR % LPP == 0 && NRL >= 1 && NRL <= 8), "remainder shape");
+  static_assert(NR == 0 || (!BF && NR <= 8), "remainder shape");
   __shared__ float red[NW][2][BNT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
@@ -770,19 +767,20 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   };
-  // VALU remainder: this lane's pixel (same tile rows / columns as the MFMA A rows) and
-  // channel group; its accumulators; the slab's remainder weights rw[NR][9][cs4*4] in LDS
-  const int rl = lane % PPW, rh = lane / PPW;
-  const int rtrow = wave * (TM / 2) + ((rl >> 4) >> 1), rtcol = ((rl >> 4) & 1) * 16 + (rl & 15);
-  const int rbase = ((rtrow + 1) * LW + rtcol + 1) * csp;
+  // VALU remainder: lane (g, r) multiplies the A fragments it already holds (pixels
+  // i*16 + r of its TM row tiles, the 4 channels of K step 4c + g) with that K step's
+  // remainder weights; the 4 lane groups' shares are summed at the end.  The slab's
+  // remainder weights rw[NR][(tap, quad) step][4] live in LDS.
   float* const rw = tile + LH * LW * csp;
   // floats per remainder channel in rw: the K steps of an even number of chunks (the main
   // loop runs chunks in pairs), zero past the slab's 9 x qs steps
   const int rws = ((9 * p.cs4 + 7) >> 3) * 32;
   int2* const tab = reinterpret_cast<int2*>(rw + NR * rws);
-  float racc[NRL > 0 ? NRL : 1];
+  float racc[TM][NR > 0 ? NR : 1];
 #pragma unroll
-  for (int j = 0; j < NRL; ++j) racc[j] = 0.f;
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) racc[i][j] = 0.f;
 
   const int img_base = img * p.img_h;
   for (int q0 = 0; q0 < Q; q0 += p.cs4) {
@@ -879,27 +877,24 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + (uint32_t)e.y);
     };
-    // the remainder's share of a chunk: its 4 K steps, A offsets from the same table
-    // (wave-uniform; steps past the 9 taps read tap 0 against the zeroed tail of rw)
-    int rkq = 0;
-    auto rem = [&]() {
+    // the remainder's share of a chunk: this lane's K step (4c + g) against the A
+    // fragments of the MFMAs (steps past the 9 taps meet the zeroed tail of rw)
+    int rch = 0;
+    auto rem = [&](const f4* fa) {
       if constexpr (NR > 0) {
-        const int4 o4 = reinterpret_cast<const int4*>(tab)[rkq >> 1];
-        const int4 o5 = reinterpret_cast<const int4*>(tab)[(rkq >> 1) + 1];
-        const int xo[4] = {o4.x, o4.z, o5.x, o5.z};
+        const int ks = 4 * rch + g;
+        ++rch;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f4 xv = *reinterpret_cast<const f4*>(&tile[rbase + xo[u]]);
+        for (int j = 0; j < NR; ++j) {
+          const f4 wv = *reinterpret_cast<const f4*>(&rw[j * rws + 4 * ks]);
 #pragma unroll
-          for (int j = 0; j < NRL; ++j) {
-            const f4 wv = *reinterpret_cast<const f4*>(&rw[(rh * NRL + j) * rws + 4 * (rkq + u)]);
-            racc[j] = __builtin_fmaf(xv[0], wv[0], racc[j]);
-            racc[j] = __builtin_fmaf(xv[1], wv[1], racc[j]);
-            racc[j] = __builtin_fmaf(xv[2], wv[2], racc[j]);
-            racc[j] = __builtin_fmaf(xv[3], wv[3], racc[j]);
+          for (int i = 0; i < TM; ++i) {
+            racc[i][j] = __builtin_fmaf(fa[i][0], wv[0], racc[i][j]);
+            racc[i][j] = __builtin_fmaf(fa[i][1], wv[1], racc[i][j]);
+            racc[i][j] = __builtin_fmaf(fa[i][2], wv[2], racc[i][j]);
+            racc[i][j] = __builtin_fmaf(fa[i][3], wv[3], racc[i][j]);
           }
         }
-        rkq += 4;
       }
     };
     if (!BF) {
@@ -907,10 +902,10 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       for (int ch = 0; ch < nch; ch += 2) {
         load(fa1, fb1);
         mma(fa0, fb0);
-        rem();
+        rem(fa0);
         load(fa0, fb0);
         mma(fa1, fb1);
-        rem();
+        rem(fa1);
       }
     } else {  // bf16 operands: one 16x16x32 MFMA per chunk pair
       load(fa0, fb0);
@@ -1054,30 +1049,43 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       }
     }
   }
-  // the VALU remainder's outputs: NRL consecutive channels of this lane's pixel
-  float rsum[NRL > 0 ? NRL : 1], rsq[NRL > 0 ? NRL : 1];
+  // the VALU remainder's outputs: the 4 lane groups' K-step shares summed (every group
+  // then holds pixel i*16 + r's sums); lane group g writes the channels j = g (mod 4)
+  float rsum[NR > 0 ? NR : 1], rsq[NR > 0 ? NR : 1];
   if constexpr (NR > 0) {
-    const int oh = oh0 + rtrow, ow = ow0 + rtcol;
-    const bool in = oh < p.img_h && ow < p.img_w;
-    const int nb = n0 + BN + rh * NRL;
-    const int64_t pix = (int64_t)(img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0);
-    float* yrow = p.y + pix * p.y_ps + nb;
 #pragma unroll
-    for (int j = 0; j < NRL; ++j) {
-      float v = racc[j];
-      if (p.bias) v += p.bias[nb + j];
-      if (p.beta != 0.f && in) v += p.beta * yrow[j];
-      if (in && (!(VAE2_ABLATE & 2) || v == 1234.5f)) yrow[j] = v;
-      if (bnp) {
-        const int n = nb + j;
-        const float xv = in ? p.bx[pix * p.bx_ps + n] : 0.f;
-        const float gv = (p.brelu && !(__builtin_fmaf(xv, p.bsave[2 * p.n + n],
-                                                      p.bsave[3 * p.n + n]) > 0.f)) ? 0.f : v;
-        rsum[j] = in ? gv : 0.f;
-        rsq[j] = in ? gv * (xv - p.bsave[n]) * p.bsave[p.n + n] : 0.f;
-      } else {
-        rsum[j] = in ? v : 0.f;
-        rsq[j] = in ? v * v : 0.f;
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        racc[i][j] += __shfl_xor(racc[i][j], 16, 64);
+        racc[i][j] += __shfl_xor(racc[i][j], 32, 64);
+      }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      rsum[j] = 0.f;
+      rsq[j] = 0.f;
+      if ((j & 3) != g) continue;
+      const int n = n0 + BN + j;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int oh = oh0 + wave * (TM / 2) + (i >> 1), ow = ow0 + (i & 1) * 16 + r;
+        const bool in = oh < p.img_h && ow < p.img_w;
+        const int64_t pix = (int64_t)(img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0);
+        float* yp = p.y + pix * p.y_ps + n;
+        float v = racc[i][j];
+        if (p.bias) v += p.bias[n];
+        if (p.beta != 0.f && in) v += p.beta * *yp;
+        if (in && (!(VAE2_ABLATE & 2) || v == 1234.5f)) *yp = v;
+        if (bnp) {
+          const float xv = in ? p.bx[pix * p.bx_ps + n] : 0.f;
+          const float gv = (p.brelu && !(__builtin_fmaf(xv, p.bsave[2 * p.n + n],
+                                                        p.bsave[3 * p.n + n]) > 0.f)) ? 0.f : v;
+          rsum[j] += in ? gv : 0.f;
+          rsq[j] += in ? gv * (xv - p.bsave[n]) * p.bsave[p.n + n] : 0.f;
+        } else {
+          rsum[j] += in ? v : 0.f;
+          rsq[j] += in ? v * v : 0.f;
+        }
       }
     }
   }
@@ -1096,20 +1104,21 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         red[wave][1][j * 16 + r] = csq[j];
       }
     }
-    if constexpr (NR > 0) {  // sum over the wave's pixels (lanes of one channel group)
+    if constexpr (NR > 0) {  // sum over the wave's pixels (the 16 lanes r of group g)
 #pragma unroll
-      for (int j = 0; j < NRL; ++j) {
+      for (int j = 0; j < NR; ++j) {
 #pragma unroll
-        for (int o = 1; o < PPW; o <<= 1) {
+        for (int o = 1; o < 16; o <<= 1) {
           rsum[j] += __shfl_xor(rsum[j], o, 64);
           rsq[j] += __shfl_xor(rsq[j], o, 64);
         }
       }
-      if (rl == 0) {
+      if (r == 0) {
 #pragma unroll
-        for (int j = 0; j < NRL; ++j) {
-          red[wave][0][BN + rh * NRL + j] = rsum[j];
-          red[wave][1][BN + rh * NRL + j] = rsq[j];
+        for (int j = 0; j < NR; ++j) {
+          if ((j & 3) != g) continue;
+          red[wave][0][BN + j] = rsum[j];
+          red[wave][1][BN + j] = rsq[j];
         }
       }
     }
@@ -1185,9 +1194,12 @@ int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persisten
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
 int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
 int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
-int g_wgrad_cols = 0;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
+// (keys 1 and 3 on by default: round-4 A/B on one box, 20-step benches twice interleaved:
+//  default 820.7 / 822.4 frames/s, key 1 824.2 / 823.1, key 3 828.3 / 828.3; key 2 (8-wave
+//  direct 3x3) 825.1 / 823.8 and key 0 = 1024 819.7 / 818.4 stay off)
+int g_wgrad_cols = 1;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
 int g_dconv_nw8 = 0;      // vae2_conv2d_set_tune key 2: direct 3x3 8-row tiles as 8 waves
-int g_wgrad_nw8 = 0;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients over 8 waves
+int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients over 8 waves
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8;

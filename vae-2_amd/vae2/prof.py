@@ -117,10 +117,33 @@ def fwd_kernel_name(xa, yshape, k, stride, pad):
     return buf.value.decode()
 
 
+_SLEEP_RATE = {}
+
+
+def _sleep_cycles(us):
+    """torch.cuda._sleep argument that spins the stream for about `us` microseconds
+    (calibrated once per device against HIP events)."""
+    dev = torch.cuda.current_device()
+    rate = _SLEEP_RATE.get(dev)
+    if rate is None:
+        n = 1 << 20
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(n)  # warm
+        a.record()
+        torch.cuda._sleep(n)
+        b.record()
+        b.synchronize()
+        ms = a.elapsed_time(b)
+        rate = n / max(ms * 1e3, 1e-3)  # cycles per microsecond
+        _SLEEP_RATE[dev] = rate
+    return max(int(us * rate), 1)
+
+
 class StepProfiler:
-    def __init__(self):
+    def __init__(self, lead_us=40.0):
         self.records = []  # (abi fn, kernels label, start ev, end ev, flops, bytes, shape)
         self.pending = None
+        self.lead_cycles = _sleep_cycles(lead_us) if lead_us else 0
         self.conflicts = 0  # notes overwritten before their call (must stay 0)
         self._buf = ctypes.create_string_buffer(1 << 14)
 
@@ -145,6 +168,12 @@ class StepProfiler:
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         lib.vae2_kernel_log_read(None, 0)  # drop launches made outside annotated calls
+        # keep the stream busy while the host queues the start event, the call's kernels
+        # and the end event: the bracket then holds the kernels' execution, not the host's
+        # launch latency (the eager profiled step is host-bound, so without it every short
+        # kernel's span included the gap before its launch)
+        if self.lead_cycles:
+            torch.cuda._sleep(self.lead_cycles)
         s.record(cur)
         rc = fn(*args)
         e.record(cur)
