@@ -23,7 +23,7 @@ for i in $IDX; do
   done
 done
 python vae-2_amd/tools/sq_summary.py gpurun_out ${TAG} > gpurun_out/${TAG}_summary.json || exit 1
-for b in 2 4 8 16 32; do
+for b in 4 8 16; do
   timeout -k 10 120 python vae-2_amd/tools/conv_bench.py --only $IDX --batch $b --iters 20 \
     > gpurun_out/${TAG}_batch$b.log 2>&1 || { tail -5 gpurun_out/${TAG}_batch$b.log; exit 1; }
   echo "B=$b"; grep -E "^[0-9]+x[0-9]+" gpurun_out/${TAG}_batch$b.log
