@@ -85,6 +85,8 @@ def parse():
                          "(vae2.ops.LazyBN; A/B)")
     ap.add_argument("--conv-algo", type=int, default=None,
                     help="vae2_conv2d_set_algo bits (A/B of kernel choices; default: auto)")
+    ap.add_argument("--heads-algo", type=int, default=None,
+                    help="vae2_heads_set_algo value (A/B of the head kernel variants)")
     ap.add_argument("--conv-tune", default="",
                     help="vae2_conv2d_set_tune key=value[,key=value] (launch-shape A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
@@ -242,6 +244,9 @@ def main():
     if args.conv_grouping == "on":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_grouping(1)
+    if args.heads_algo is not None:
+        from vae2 import _lib
+        _lib.load().vae2_heads_set_algo(args.heads_algo)
     if args.conv_algo is not None:
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_algo(args.conv_algo)

@@ -130,8 +130,8 @@ def test_heads_packed_cols_follow_optimizer_updates():
 @pytest.mark.parametrize("hw,n", [((64, 128), 2), ((32, 64), 3)])
 def test_upsample_adjoint_streaming_equals_lane_kernel(hw, n):
     """The row-streaming vertical pass of the power-of-two upsampling adjoint
-    (up_adj2_vs_kernel) against the per-channel-lane one (vae2_heads_set_algo bit 0):
-    same weights, same summation order."""
+    (up_adj2_vs_kernel) against the per-channel-lane one (vae2_heads_set_algo bit 0), both
+    in the two-pass form (bit 2): same weights, same summation order."""
     from vae2 import _lib
     from vae2 import heads as vheads
     heads, ys = _heads_and_inputs("w18", hw, n)
@@ -139,7 +139,7 @@ def test_upsample_adjoint_streaming_equals_lane_kernel(hw, n):
     grads = []
     lib = _lib.load()
     try:
-        for algo in (0, 1):
+        for algo in (4, 5):
             lib.vae2_heads_set_algo(algo)
             hip_h = [copy.deepcopy(h).to(DEV) for h in heads]
             ys_hip = [y.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_() for y in ys]
@@ -153,3 +153,50 @@ def test_upsample_adjoint_streaming_equals_lane_kernel(hw, n):
         lib.vae2_heads_set_algo(0)
     for a, b in zip(*grads):
         assert max_rel(a, b) < 1e-6, max_rel(a, b)
+
+
+@pytest.mark.parametrize("n,c,H,W,nsrc", [(2, 270, 64, 128, 3), (1, 70, 8, 64, 3),
+                                          (1, 18, 96, 192, 3), (2, 36, 40, 128, 2),
+                                          (1, 20, 34, 64, 1), (3, 64, 32, 64, 3)])
+def test_upsample_adjoint_multi_against_fp64(n, c, H, W, nsrc):
+    """vae2_upsample_bilinear_bwd_multi (the heads' dL/dz_j = up_j^T(dL/dy)) against
+    torch's fp64 autograd of F.interpolate(bilinear, align_corners=False)
+    (enc_hrnet.py:839-845): the one-pass band kernel at its default and at 8 / 64 dy rows
+    per workgroup, and the two-pass form (vae2_heads_set_algo bit 2).  Shapes cover one
+    band, several bands, a last band shorter than the others, 1-row coarsest targets (both
+    vertical folds in one row) and pad channels (c % 64 != 0)."""
+    import ctypes
+    from vae2 import _lib, ops
+    from vae2._lib import Act, call
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(H * W + c)
+    dy = torch.randn(n, c, H, W, generator=g, dtype=torch.float64)
+    refs = []
+    for s in range(nsrc):
+        z = torch.zeros(n, c, H >> (s + 1), W >> (s + 1), dtype=torch.float64,
+                        requires_grad=True)
+        F.interpolate(z, size=(H, W), mode="bilinear", align_corners=False).backward(dy)
+        refs.append(z.grad)
+    gt = ops.new_act((n, H, W, c), torch.empty(0, device=DEV))
+    gt.copy_(dy.float().permute(0, 2, 3, 1))
+    gp, ga = ops.act_of(gt)
+    try:
+        for algo in (0, 8 << 8, 64 << 8, 4):
+            lib.vae2_heads_set_algo(algo)
+            dxs = [ops.new_act((n, H >> (s + 1), W >> (s + 1), c), gt) for s in range(nsrc)]
+            for d in dxs:
+                d.fill_(float("nan"))  # every target element must be written
+            views = [ops.act_of(d) for d in dxs]
+            acts = (Act * 3)(*[a for _, a in views])
+            ptrs = (ctypes.c_void_p * 3)(*[p for p, _ in views])
+            wsz = lib.vae2_upsample_bilinear_bwd_multi_ws_size(ctypes.byref(ga), nsrc, acts)
+            ws = torch.empty(max(wsz, 1), device=DEV)
+            call("vae2_upsample_bilinear_bwd_multi", gp, ctypes.byref(ga), nsrc, ptrs, acts,
+                 ws.data_ptr(), wsz, None)
+            torch.cuda.synchronize()
+            for d, r in zip(dxs, refs):
+                got = d.permute(0, 3, 1, 2).double().cpu()
+                assert torch.isfinite(got).all(), algo
+                assert max_rel(got, r) < 2e-6, (algo, max_rel(got, r))
+    finally:
+        lib.vae2_heads_set_algo(0)

@@ -850,6 +850,160 @@ __global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) 
   }
 }
 
+// One-pass form of the power-of-two adjoint: dx_s = V_s^T H_s^T dy for every source with
+// dy read once (plus a row halo) and no hb intermediate (the two-pass form above writes and
+// re-reads 1/2 + 1/4 + 1/8 of dy).  Workgroup = (image, band of `br` dy rows, 64-pixel
+// chunk, 64-channel block); lane = channel; wave w owns the source columns whose pixels
+// start in [x0 + 16w, x0 + 16w + 16): 16/F per source.  The band's dy rows plus HF_max rows
+// above and below stream through registers (the next row's loads in flight during the
+// current row's arithmetic).  A dy row oy feeds exactly two target rows of source s,
+// ih = (oy + HF) / F and ih - 1 (taps d = oy - F*ih and d + F); per source and owned column
+// two accumulators follow them, and a row is stored once oy has moved past it.  Virtual
+// rows / columns -1 and z are folded into 0 / z-1 as in up_adj2_h / up_adj2_vs, with the
+// same hat_w weights; interior outputs keep the two-pass summation order.
+static int g_adj_fused = 1;  // vae2_heads_set_algo bit 2 clears it
+static int g_adj_band = 32;  // dy rows per workgroup (a multiple of 8)
+
+// Logical block order with consecutive ids on one XCD (the hardware deals workgroups out
+// round-robin over the 8 XCDs): neighbouring chunks / bands share dy halo rows in that L2.
+__device__ __forceinline__ int xcd_remap_blocks(int orig, int n) {
+  const int q = n >> 3, rr = n & 7, x = orig & 7;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (orig >> 3);
+}
+
+// Per-source state of up_adj3_kernel: the wave's 16/F owned columns in the two target rows
+// the current dy row feeds (lo = ih - 1, hi = ih), cur = ih.
+template <int S>
+struct Adj3Src {
+  static constexpr int F = 2 << S, HF = 1 << S, J = 8 >> S;
+  float lo[J], hi[J];
+  int cur;
+};
+
+template <int S>
+__device__ __forceinline__ void adj3_store(const Adj3Src<S>& a, const UpAdj& p, int n, int iy,
+                                           int b0, int b1, int px0, int c, bool cok) {
+  constexpr int F = Adj3Src<S>::F;
+  if (!cok || iy < b0 / F || iy >= b1 / F) return;
+  float* out = p.dx[S] + ((int64_t)n * p.zh[S] + iy) * p.zw[S] * p.dx_ps[S] + c;
+  const int ix0 = px0 / F;
+#pragma unroll
+  for (int j = 0; j < Adj3Src<S>::J; ++j) out[(int64_t)(ix0 + j) * p.dx_ps[S]] = a.lo[j];
+}
+
+// dy row oy (pixels px0 - HM + i in v[i]) into source S's accumulators.
+template <int S, int HM>
+__device__ __forceinline__ void adj3_row(Adj3Src<S>& a, const float* v, int oy, const UpAdj& p,
+                                         int n, int b0, int b1, int px0, int c, bool cok) {
+  constexpr int F = Adj3Src<S>::F, HF = Adj3Src<S>::HF, J = Adj3Src<S>::J;
+  const int ih = (oy + HF) >> (S + 1);
+  if (ih != a.cur) {  // target row cur - 1 is complete
+    adj3_store<S>(a, p, n, a.cur - 1, b0, b1, px0, c, cok);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      a.lo[j] = a.hi[j];
+      a.hi[j] = 0.f;
+    }
+    a.cur = ih;
+  }
+  const int d = oy - F * ih;
+  const float wh = hat_w(d, F), wl = hat_w(d + F, F);
+  const int zw = p.zw[S], ix0 = px0 / F;
+  const int mode = ih == p.zh[S] ? 2 : ih == 0 ? 1 : 0;  // 2: row zh folds into zh - 1; 1: -1 into 0
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const float* vj = v + HM + F * j;  // pixel px0 + F*j
+    float h = 0.f;
+#pragma unroll
+    for (int dd = -HF; dd < 3 * HF; ++dd) h += hat_w(dd, F) * vj[dd];
+    if (ix0 + j == 0) {  // virtual column -1 (pixels dd - F)
+#pragma unroll
+      for (int dd = F; dd < 3 * HF; ++dd) h += hat_w(dd, F) * vj[dd - F];
+    }
+    if (ix0 + j == zw - 1) {  // virtual column zw (pixels F*(j+1) + dd)
+#pragma unroll
+      for (int dd = -HF; dd < 0; ++dd) h += hat_w(dd, F) * vj[F + dd];
+    }
+    if (mode == 2) {
+      a.lo[j] += wh * h;
+      a.lo[j] += wl * h;
+    } else if (mode == 1) {
+      a.hi[j] += wh * h;
+      a.hi[j] += wl * h;
+    } else {
+      a.hi[j] += wh * h;
+      a.lo[j] += wl * h;
+    }
+  }
+}
+
+template <int NUP>
+__global__ __launch_bounds__(256) void up_adj3_kernel(UpAdj p, int br, int nband) {
+  constexpr int HM = 1 << (NUP - 1);  // row / pixel halo: HF of the coarsest source
+  constexpr int NV = 16 + 2 * HM;     // dy pixels per wave and row
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncb = (p.C + 63) >> 6;
+  const int lb = xcd_remap_blocks(blockIdx.x, gridDim.x);
+  const int xb = lb % p.nxb;
+  int t = lb / p.nxb;
+  const int cbi = t % ncb;
+  t /= ncb;
+  const int band = t % nband, n = t / nband;
+  const int c = cbi * 64 + lane;
+  const bool cok = c < p.C;
+  const int b0 = band * br, b1 = b0 + br < p.H ? b0 + br : p.H;
+  const int ys = b0 - HM > 0 ? b0 - HM : 0, ye = b1 + HM < p.H ? b1 + HM : p.H;
+  const int px0 = xb * kUsXB + 16 * wave;
+  // One buffer resource per dy row (num_records = the row's bytes): pixels left of the row
+  // wrap to huge offsets and pixels right of it exceed the row, so both load 0 with no
+  // per-pixel test; pad channels use an offset past any row.
+  const uint32_t pstep = (uint32_t)p.dy_ps * 4u, rbytes = (uint32_t)p.W * pstep;
+  const uint32_t loff = cok ? (uint32_t)(px0 - HM) * pstep + 4u * (uint32_t)c : kOOB;
+  const float* img = p.dy + (int64_t)n * p.H * p.W * p.dy_ps;
+  auto load_row = [&](int oy, float* dst) {
+    const __amdgpu_buffer_rsrc_t dr = make_rsrc(img + (int64_t)oy * p.W * p.dy_ps, rbytes);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dst[i] = load1(dr, loff + (uint32_t)i * pstep);
+  };
+  Adj3Src<0> a0;
+  Adj3Src<1> a1;
+  Adj3Src<2> a2;
+  a0.cur = (ys + 1) >> 1;
+  a1.cur = (ys + 2) >> 2;
+  a2.cur = (ys + 4) >> 3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a0.lo[j] = a0.hi[j] = 0.f;
+    if (j < 4) a1.lo[j] = a1.hi[j] = 0.f;
+    if (j < 2) a2.lo[j] = a2.hi[j] = 0.f;
+  }
+  float v[NV], nv[NV];
+  load_row(ys, v);
+  for (int oy = ys; oy < ye; ++oy) {
+    if (oy + 1 < ye) load_row(oy + 1, nv);
+    adj3_row<0, HM>(a0, v, oy, p, n, b0, b1, px0, c, cok);
+    if constexpr (NUP > 1) adj3_row<1, HM>(a1, v, oy, p, n, b0, b1, px0, c, cok);
+    if constexpr (NUP > 2) adj3_row<2, HM>(a2, v, oy, p, n, b0, b1, px0, c, cok);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = nv[i];
+  }
+  adj3_store<0>(a0, p, n, a0.cur - 1, b0, b1, px0, c, cok);
+  if constexpr (NUP > 1) adj3_store<1>(a1, p, n, a1.cur - 1, b0, b1, px0, c, cok);
+  if constexpr (NUP > 2) adj3_store<2>(a2, p, n, a2.cur - 1, b0, b1, px0, c, cok);
+}
+
+// The one-pass adjoint applies: exact 2^(s+1) ratios, 64-pixel chunks, rows addressable
+// with 32-bit buffer offsets.
+static bool adj_one_pass(const vae2_act* dyd, int n, const vae2_act* dxds) {
+  if (!g_adj_fused || n < 1 || dyd->w % kUsXB != 0 || dyd->w * dyd->ps * 4 >= (int64_t)kOOB)
+    return false;
+  for (int s = 0; s < n; ++s)
+    if (!act_ok(&dxds[s]) || dyd->w != dxds[s].w << (s + 1) || dyd->h != dxds[s].h << (s + 1))
+      return false;
+  return true;
+}
+
 // Pixels per block of the backward passes (>= 64 each): the reduce pass with <= 2048
 // blocks (a block holds only 3 pixel rows of 68 channel quads, so 1024 blocks left one
 // wave per SIMD: 134 -> 122 us per head), the apply pass with <= 1024 (measured better).
@@ -1024,15 +1178,20 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
 int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
                                                  const vae2_act* dxds) {
   if (!act_ok(dyd) || n < 0 || n > 3 || (n && !dxds)) return 0;
+  if (adj_one_pass(dyd, n, dxds)) return 1;  // no hb intermediate
   int64_t t = 0;
   for (int s = 0; s < n; ++s) t += dyd->n * dyd->h * dxds[s].w * dyd->c;
   return t > 0 ? t : 1;
 }
 
 int vae2_heads_set_algo(int algo) {
-  const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2);
+  const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2) | (g_adj_fused ? 0 : 4) |
+                   (g_adj_band == 32 ? 0 : g_adj_band << 8);
   g_adj_stream = (algo & 1) ? 0 : 1;
   g_upsum_tight = (algo & 2) ? 0 : 1;
+  g_adj_fused = (algo & 4) ? 0 : 1;
+  const int band = (algo >> 8) & 0xff;  // one-pass adjoint band rows (0: default 32)
+  g_adj_band = band >= 8 && band % 8 == 0 ? band : 32;
   return prev;
 }
 
@@ -1067,6 +1226,17 @@ int vae2_upsample_bilinear_bwd_multi(const float* dy, const vae2_act* dyd, int n
   bool pow2 = dyd->w % kUsXB == 0;
   for (int s = 0; s < n; ++s)
     pow2 = pow2 && dyd->w == (int64_t)p.zw[s] << (s + 1) && dyd->h == (int64_t)p.zh[s] << (s + 1);
+  if (adj_one_pass(dyd, n, dxds)) {
+    const int br = dyd->h < g_adj_band ? (int)dyd->h : g_adj_band;
+    const int nband = (int)ceil_div(dyd->h, br);
+    const dim3 grid((unsigned)(dyd->n * nband * p.nxb * cb));
+    switch (n) {
+      case 1: VAE2_LAUNCH(up_adj3_kernel<1>, grid, dim3(256), 0, st, p, br, nband); break;
+      case 2: VAE2_LAUNCH(up_adj3_kernel<2>, grid, dim3(256), 0, st, p, br, nband); break;
+      default: VAE2_LAUNCH(up_adj3_kernel<3>, grid, dim3(256), 0, st, p, br, nband); break;
+    }
+    return check_launch(fn);
+  }
   if (pow2) {
     const dim3 grid((unsigned)(dyd->n * dyd->h * p.nxb * cb));
     switch (n) {

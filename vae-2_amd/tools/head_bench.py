@@ -77,7 +77,9 @@ def main():
     gs = [new_act((n, h, w_, C), ys[0]) for (h, w_) in sizes[1:]]
     gptrs = (ctypes.c_void_p * 3)(*[act_of(g)[0] for g in gs])
     gacts = (Act * 3)(*[act_of(g)[1] for g in gs])
+    lib.vae2_heads_set_algo(4)  # the two-pass form's workspace (the largest)
     usz = lib.vae2_upsample_bilinear_bwd_multi_ws_size(ctypes.byref(ya), 3, gacts)
+    lib.vae2_heads_set_algo(0)
     uws = torch.empty(usz, device=dev)
 
     ynp, yna = act_of(new_act((n, H, W, C), ys[0]).normal_())
@@ -85,9 +87,13 @@ def main():
     def adj():
         call("vae2_upsample_bilinear_bwd_multi", ynp, ctypes.byref(yna), 3, gptrs, gacts, ptr(uws),
              usz, s)
-    res.append(("upsample adjoint x3 (dy read + dx write)", timeit(adj, a.iters), P * C * 4 + zb))
-    lib.vae2_heads_set_algo(1)
-    res.append(("  same, per-channel-lane vertical pass", timeit(adj, a.iters), P * C * 4 + zb))
+    for algo, name in ((0, "upsample adjoint x3, one pass (dy read + dx write)"),
+                       (16 << 8, "  same, 16 dy rows per workgroup"),
+                       (64 << 8, "  same, 64 dy rows per workgroup"),
+                       (4, "  two-pass (horizontal -> hb -> vertical)"),
+                       (5, "  two-pass, per-channel-lane vertical pass")):
+        lib.vae2_heads_set_algo(algo)
+        res.append((name, timeit(adj, a.iters), P * C * 4 + zb))
     lib.vae2_heads_set_algo(0)
 
     save = torch.cat([torch.zeros(C), torch.ones(C), torch.ones(C), torch.zeros(C)]).to(dev)

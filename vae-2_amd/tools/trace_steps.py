@@ -45,7 +45,7 @@ def load(path):
     return rows
 
 
-def select_steps(rows, steps, marker="adam"):
+def select_steps(rows, steps, marker="adam", skip=0):
     marks = [i for i, r in enumerate(rows) if marker in r[2]]
     ends = []  # group consecutive marker launches of one step (several flats)
     for i in marks:
@@ -53,6 +53,8 @@ def select_steps(rows, steps, marker="adam"):
             ends[-1] = i
         else:
             ends.append(i)
+    if skip:
+        ends = ends[:-skip]
     if len(ends) < steps + 1:
         raise SystemExit(f"only {len(ends)} steps found")
     return rows[ends[-steps - 1] + 1:ends[-1] + 1]
@@ -95,9 +97,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--marker", default="adam")
     ap.add_argument("--instances", type=int, default=25)
+    ap.add_argument("--skip", type=int, default=0,
+                    help="leave out the last N steps (bench.py's eager roofline steps: the "
+                         "graph-replayed timed steps come before them)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    b = breakdown(select_steps(load(a.csv), a.steps, a.marker), a.steps)
+    b = breakdown(select_steps(load(a.csv), a.steps, a.marker, a.skip), a.steps)
     print(f"steps {b['steps']}: wall/step {b['wall_ms_per_step']:.2f} ms, busy/step "
           f"{b['busy_ms_per_step']:.2f} ms, summed kernel/step {b['kernel_ms_per_step']:.2f} ms, "
           f"launches/step {b['launches_per_step']:.0f}")
