@@ -14,7 +14,7 @@ timeout -k 10 120 python vae-2_amd/tools/head_bench.py > gpurun_out/${TAG}_hb.lo
 cat gpurun_out/${TAG}_hb.log
 i=0
 for rep in 1 2; do
-  for v in 0 4; do
+  for v in 0 ${ALT:-4}; do
     i=$((i+1))
     timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline --steps 20 --heads-algo $v \
       > gpurun_out/${TAG}_ab_$i.log 2>&1 || { tail -5 gpurun_out/${TAG}_ab_$i.log; exit 1; }

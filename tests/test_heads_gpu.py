@@ -200,3 +200,62 @@ def test_upsample_adjoint_multi_against_fp64(n, c, H, W, nsrc):
                 assert max_rel(got, r) < 2e-6, (algo, max_rel(got, r))
     finally:
         lib.vae2_heads_set_algo(0)
+
+
+@pytest.mark.parametrize("n,H,W,cin,nup", [(2, 64, 128, 18, 3), (1, 128, 256, 18, 3),
+                                           (2, 32, 64, 7, 2), (1, 16, 64, 4, 1)])
+def test_upsum_one_pass_against_fp64(n, H, W, cin, nup):
+    """vae2_conv1x1_upsum_fwd's one-pass kernel (upsum2_kernel: W0 x0 on MFMA, source rows
+    in registers) and the LDS-staged one (vae2_heads_set_algo bit 3) against fp64 of
+    y = W0 x0 + b + sum_j up(z_j) (enc_hrnet.py:839-847 with the 1x1 conv commuted),
+    and the shifted BN statistics rows of y - b summed over rows."""
+    import ctypes
+    from vae2 import _lib, ops
+    from vae2._lib import Act, call
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(n * H + cin)
+    C = 270
+    x0 = torch.randn(n, cin, H, W, generator=g, dtype=torch.float64)
+    zs = [torch.randn(n, C, H >> (s + 1), W >> (s + 1), generator=g, dtype=torch.float64)
+          for s in range(nup)]
+    w = torch.randn(C, cin, generator=g, dtype=torch.float64) / cin ** 0.5
+    b = torch.randn(C, generator=g, dtype=torch.float64)
+    ref = torch.einsum("ck,nkhw->nchw", w, x0)
+    for z in zs:
+        ref = ref + F.interpolate(z, size=(H, W), mode="bilinear", align_corners=False)
+    s1, s2 = ref.sum((0, 2, 3)), (ref * ref).sum((0, 2, 3))
+    ref = ref + b[None, :, None, None]
+    dev = torch.empty(0, device=DEV)
+    xa = ops.new_act((n, H, W, cin), dev)
+    xa.copy_(x0.float().permute(0, 2, 3, 1))
+    xp, xd = ops.act_of(xa)
+    za = []
+    for z in zs:
+        t = ops.new_act((n, z.shape[2], z.shape[3], C), dev)
+        t.copy_(z.float().permute(0, 2, 3, 1))
+        za.append(t)
+    wd = w.float().to(DEV).contiguous()
+    wp = torch.empty(lib.vae2_conv2d_packed_size(C, cin, 1, 0), device=DEV)
+    call("vae2_conv2d_pack_weight_ld", ops.ptr(wd), C, cin, 1, 0, cin, ops.ptr(wp), None)
+    bd = b.float().to(DEV)
+    ya = Act(n, H, W, C, C)
+    rows = lib.vae2_conv1x1_upsum_stats_rows(ctypes.byref(ya))
+    ups = (ctypes.c_void_p * 3)(*[ops.act_of(t)[0] for t in za])
+    upds = (Act * 3)(*[ops.act_of(t)[1] for t in za])
+    ncb = -(-C // 64)
+    try:
+        for algo in (0, 8):
+            lib.vae2_heads_set_algo(algo)
+            y = torch.full((ncb * n * H * W * 64,), float("nan"), device=DEV)
+            stats = torch.empty(2 * rows * C, device=DEV)
+            call("vae2_conv1x1_upsum_fwd", xp, ctypes.byref(xd), ops.ptr(wp), ops.ptr(bd), nup,
+                 ups, upds, ops.ptr(y), ctypes.byref(ya), ops.ptr(stats), None)
+            torch.cuda.synchronize()
+            got = y.view(ncb, n, H, W, 64).permute(1, 0, 4, 2, 3).reshape(n, ncb * 64, H, W)
+            got = got[:, :C].double().cpu()
+            assert max_rel(got, ref) < 1e-5, (algo, max_rel(got, ref))
+            st = stats.view(2, rows, C).double().sum(1).cpu()
+            assert max_rel(st[0], s1) < 1e-4, (algo, max_rel(st[0], s1))
+            assert max_rel(st[1], s2) < 1e-5, (algo, max_rel(st[1], s2))
+    finally:
+        lib.vae2_heads_set_algo(0)

@@ -19,6 +19,19 @@ namespace vae2 {
 
 
 constexpr int kHeadMaxOut = 4;
+constexpr int64_t kHeadMaxPpb = 2048;  // pixels per block of the backward passes (LDS dout)
+
+// The block's dout rows [p0, p1) x CO, staged once in LDS (every channel quad of a pixel
+// reads the same CO values: one coalesced pass instead of CO scalar loads per quad)
+template <int CO>
+__device__ __forceinline__ void head_stage_dout(float* sd, const float* dout, const Act& dod,
+                                                int64_t p0, int64_t p1) {
+  const int n = (int)(p1 - p0) * CO;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int pp = i / CO, o = i - pp * CO;
+    sd[i] = dout[(p0 + pp) * dod.ps + o];
+  }
+}
 
 __device__ __forceinline__ f4 hld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
@@ -122,7 +135,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
     const float* __restrict__ y, Act yd, const float* __restrict__ save,
     const float* __restrict__ w2, const float* __restrict__ dout, Act dod, int64_t ppb,
     int rows, float* __restrict__ part) {
-  extern __shared__ float red[];  // [rows][NC]
+  extern __shared__ float red[];  // [rows][NC], then the dout rows [ppb][CO]
   const int C = (int)yd.c, c4 = (C + 3) >> 2;
   const int NC = 2 * C + CO * C + CO;
   const int tid = threadIdx.x;
@@ -130,6 +143,9 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
   const int64_t p0 = blockIdx.x * ppb;
   const int64_t p1 = p0 + ppb < P ? p0 + ppb : P;
   const int r = tid / c4, q = tid - r * c4, c = 4 * q;
+  float* sd = red + rows * NC;
+  head_stage_dout<CO>(sd, dout, dod, p0, p1);
+  __syncthreads();
   if (tid < rows * c4) {
     const HeadCoef hc = head_coef(save, c, C);
     f4 wv[CO];
@@ -150,7 +166,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
         const bool ok = p < p1;
         vv[u] = ok ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? dout[p * dod.ps + o] : 0.f;
+        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? sd[(p - p0) * CO + o] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -244,13 +260,16 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
     const float* __restrict__ gamma, const float* __restrict__ w2,
     const float* __restrict__ dout, Act dod, const double* __restrict__ sums, double count,
     int64_t ppb, int rows, float* __restrict__ dy, Act dyd, float* __restrict__ part) {
-  extern __shared__ float red[];  // [rows][C]
+  extern __shared__ float red[];  // [rows][C], then the dout rows [ppb][CO]
   const int C = (int)yd.c, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
   const int64_t P = yd.n * yd.h * yd.w;
   const int64_t p0 = blockIdx.x * ppb;
   const int64_t p1 = p0 + ppb < P ? p0 + ppb : P;
   const int r = tid / c4, q = tid - r * c4, c = 4 * q;
+  float* sd = red + rows * C;
+  head_stage_dout<CO>(sd, dout, dod, p0, p1);
+  __syncthreads();
   if (tid < rows * c4) {
     const HeadCoef hc = head_coef(save, c, C);
     const float inv_n = (float)(1.0 / count);
@@ -275,7 +294,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
         const bool ok = p < p1;
         vv[u] = ok ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? dout[p * dod.ps + o] : 0.f;
+        for (int o = 0; o < CO; ++o) dd[u][o] = ok ? sd[(p - p0) * CO + o] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -511,6 +530,172 @@ __global__ __launch_bounds__(256) void upsum_kernel(UpSum p) {
         red[1][wave][16 * j + r] = s2[j];
       }
     }
+    __syncthreads();
+    if (wave == 0 && cok) {
+      const int rr = (n * p.nrb + oy0 / kUsRows) * p.nxb + xb;
+      p.stats[(int64_t)rr * p.C + c] =
+          (float)(red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
+      p.stats[((int64_t)p.rows + rr) * p.C + c] =
+          (float)(red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
+    }
+  }
+}
+
+// One-pass up-sum for exact 2^(s+1) sources (the HRNet heads' branches halve in size):
+// lane = channel, wave w owns pixels [x0 + 16w, x0 + 16w + 16) of the workgroup's kUsRows
+// rows, so nothing is staged in LDS and no barrier runs before the statistics.  W0 x0 is
+// computed on the VALU (K = Cin0 <= 4*KQ, 2.6 GF per head: ~10 us of VALU chip-wide) with the
+// x0 pixel -- uniform over the lanes -- in scalar registers (constant-address-space loads);
+// each source keeps its two rows of the wave's 16/F + 2 source columns in registers,
+// re-loaded only when the row pair moves (a row is loaded once per workgroup); the bilinear
+// weights are exact (integer arithmetic on pow2 ratios, compile-time horizontally).  Same
+// output layout (B64) and statistics rows (y - bias) as upsum_kernel.
+__host__ __device__ constexpr int us2_off(int pp, int F) {  // floor((pp + 0.5) / F - 0.5)
+  return 2 * pp + 1 - F >= 0 ? (2 * pp + 1 - F) / (2 * F) : -1;
+}
+__host__ __device__ constexpr float us2_frac(int pp, int F) {
+  return (float)(2 * pp + 1 - F - 2 * F * us2_off(pp, F)) / (float)(2 * F);
+}
+
+template <int S>
+struct Us2Src {
+  static constexpr int F = 2 << S, NC = 16 / F + 2;  // source columns px0/F - 1 ... px0/F + 16/F
+  float r0[NC], r1[NC];
+  int h0, h1;  // rows held in r0 / r1
+};
+
+template <int S>
+__device__ __forceinline__ void us2_rows(Us2Src<S>& a, const UpSum& p, int n, int oy, int px0,
+                                         int c, bool cok, float& l0, float& l1) {
+  constexpr int F = Us2Src<S>::F, NC = Us2Src<S>::NC;
+  const int num = 2 * oy + 1 - F;
+  const int i0 = num >= 0 ? num / (2 * F) : -1;
+  l1 = (float)(num - 2 * F * i0) / (float)(2 * F);
+  l0 = 1.f - l1;
+  const int zh = p.zh[S], zw = p.zw[S];
+  const int ra = i0 < 0 ? 0 : (i0 > zh - 1 ? zh - 1 : i0);
+  const int rb = i0 + 1 > zh - 1 ? zh - 1 : i0 + 1;
+  if (ra == a.h0 && rb == a.h1) return;
+  const __amdgpu_buffer_rsrc_t zr = make_rsrc(p.z[S], p.z_bytes[S]);
+  const int cb = px0 / F - 1;
+  auto load = [&](int row, float* dst) {
+    const int rbase = (n * zh + row) * zw;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      int col = cb + q;
+      col = col < 0 ? 0 : (col > zw - 1 ? zw - 1 : col);
+      dst[q] = load1(zr, cok ? (uint32_t)((rbase + col) * p.zps[S] + c) * 4u : kOOB);
+    }
+  };
+  if (ra == a.h1) {
+#pragma unroll
+    for (int q = 0; q < NC; ++q) a.r0[q] = a.r1[q];
+  } else {
+    load(ra, a.r0);
+  }
+  if (rb != a.h1) load(rb, a.r1);
+  a.h0 = ra;
+  a.h1 = rb;
+}
+
+template <int S>
+__device__ __forceinline__ void us2_add(const Us2Src<S>& a, float l0, float l1, float* v) {
+  constexpr int F = Us2Src<S>::F, NC = Us2Src<S>::NC;
+  float vb[NC];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) vb[q] = l0 * a.r0[q] + l1 * a.r1[q];
+#pragma unroll
+  for (int pp = 0; pp < 16; ++pp) {
+    const int o = us2_off(pp, F) + 1;
+    const float h1 = us2_frac(pp, F), h0 = 1.f - us2_frac(pp, F);
+    v[pp] += h0 * vb[o] + h1 * vb[o + 1];
+  }
+}
+
+template <int NUP, int KQ>
+__global__ __launch_bounds__(256) void upsum2_kernel(UpSum p) {
+  __shared__ double red[2][4][kUsCB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncb = (p.C + kUsCB - 1) / kUsCB;
+  const int xb = blockIdx.x % p.nxb, x0 = xb * kUsXB;
+  const int cbi = (blockIdx.x / p.nxb) % ncb;
+  const int band = blockIdx.x / (p.nxb * ncb);
+  const int n = band / p.nrb, oy0 = (band - n * p.nrb) * kUsRows;
+  const int ny = p.H - oy0 < kUsRows ? p.H - oy0 : kUsRows;
+  const int c = cbi * kUsCB + lane;
+  const bool cok = c < p.C;
+  const int px0 = x0 + 16 * wave;
+  const int g = lane >> 4, r = lane & 15;
+  // W0 fragments: B[k = 4kq + g][n = 16j + r] of the channel block (packed, zero padded)
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.wp, p.wp_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  float fb[KQ][4];
+#pragma unroll
+  for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fb[kq][j] = load1(wr, (uint32_t)((cbi * kUsCB + 16 * j + r) * p.cin4 + 4 * kq + g) * 4u);
+  __shared__ float xts[4][16 * 64];
+  float* xt = xts[wave];
+  const float bias = (p.bias && cok) ? p.bias[c] : 0.f;
+  Us2Src<0> s0;
+  Us2Src<1> s1;
+  Us2Src<2> s2;
+  s0.h0 = s0.h1 = s1.h0 = s1.h1 = s2.h0 = s2.h1 = -1;
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, p.y_bytes);
+  const int64_t P = (int64_t)(p.rows / p.nxb / p.nrb) * p.H * p.W;  // n * H * W
+  double d1 = 0.0, d2 = 0.0;
+  for (int ry = 0; ry < ny; ++ry) {
+    const int oy = oy0 + ry, row = n * p.H + oy;
+    float v[16];
+    {  // W0 x0 on MFMA (A = x0[px][k], B = W0 fragments), through this wave's LDS tile
+       // to lane = channel: lane (g, r) holds channels 16j + r of pixels 4g + e
+      f4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t xo = (uint32_t)(((row * p.W + px0 + r) * p.x_ps + g) * 4);
+#pragma unroll
+      for (int kq = 0; kq < KQ; ++kq) {
+        const float a = load1(xr, 4 * kq + g < p.cin ? xo + 16u * kq : kOOB);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, fb[kq][j], acc[j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xt[(4 * g + e) * 64 + 16 * j + r] = acc[j][e];
+#pragma unroll
+      for (int pp = 0; pp < 16; ++pp) v[pp] = xt[pp * 64 + lane];
+    }
+    float l0, l1;
+    if constexpr (NUP > 0) {
+      us2_rows<0>(s0, p, n, oy, px0, c, cok, l0, l1);
+      us2_add<0>(s0, l0, l1, v);
+    }
+    if constexpr (NUP > 1) {
+      us2_rows<1>(s1, p, n, oy, px0, c, cok, l0, l1);
+      us2_add<1>(s1, l0, l1, v);
+    }
+    if constexpr (NUP > 2) {
+      us2_rows<2>(s2, p, n, oy, px0, c, cok, l0, l1);
+      us2_add<2>(s2, l0, l1, v);
+    }
+    const uint32_t ybase = (uint32_t)(cbi * P * 64 + ((int64_t)row * p.W + px0) * 64 + lane);
+    float q1 = 0.f, q2 = 0.f;
+#pragma unroll
+    for (int pp = 0; pp < 16; ++pp) {
+      store1(yr, cok ? (ybase + pp * 64) * 4u : kOOB, v[pp] + bias);
+      q1 += v[pp];
+      q2 += v[pp] * v[pp];
+    }
+    d1 += (double)q1;
+    d2 += (double)q2;
+  }
+  if (p.stats) {
+    red[0][wave][lane] = d1;
+    red[1][wave][lane] = d2;
     __syncthreads();
     if (wave == 0 && cok) {
       const int rr = (n * p.nrb + oy0 / kUsRows) * p.nxb + xb;
@@ -805,6 +990,7 @@ __global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
 // zw * C % 4 == 0 (16-byte aligned rows).
 static int g_adj_stream = 1;  // vae2_heads_set_algo bit 0 clears it
 static int g_upsum_tight = 1;  // vae2_heads_set_algo bit 1 clears it
+static int g_upsum_one = 1;    // vae2_heads_set_algo bit 3 clears it (upsum2_kernel)
 
 template <int S>
 __global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) {
@@ -1009,7 +1195,8 @@ static bool adj_one_pass(const vae2_act* dyd, int n, const vae2_act* dxds) {
 // wave per SIMD: 134 -> 122 us per head), the apply pass with <= 1024 (measured better).
 static int64_t head_ppb(int64_t P, int64_t blocks = 2048) {
   int64_t ppb = ceil_div(P, blocks);
-  return ppb < 64 ? 64 : ppb;
+  ppb = ppb < 64 ? 64 : ppb;
+  return ppb > kHeadMaxPpb ? kHeadMaxPpb : ppb;  // the block's dout rows are staged in LDS
 }
 
 static bool head_args_ok(const float* y, const vae2_act* yd, int cout2) {
@@ -1070,7 +1257,7 @@ int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* sa
   const int NC = 2 * C + cout2 * C + cout2;
   const int64_t P = act_pixels(yd), ppb = head_ppb(P);
   const unsigned blocks = (unsigned)ceil_div(P, ppb);
-  const size_t shm = (size_t)rows * NC * sizeof(float);
+  const size_t shm = ((size_t)rows * NC + (size_t)ppb * cout2) * sizeof(float);
   VAE2_REQUIRE(shm <= 64 * 1024, fn, "too many channels for the LDS reduction");
   HEAD_DISPATCH(cout2, head_out_bwd_reduce_kernel, dim3(blocks), dim3(256), shm,
                 as_stream(stream), y, to_act(yd), save, w2, dout, to_act(doutd), ppb, rows, ws);
@@ -1098,7 +1285,7 @@ int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* sav
   const int C = (int)yd->c, c4 = (C + 3) / 4, rows = 256 / c4;
   const int64_t P = act_pixels(yd), ppb = head_ppb(P, 1024);
   const unsigned blocks = (unsigned)ceil_div(P, ppb);
-  const size_t shm = (size_t)rows * C * sizeof(float);
+  const size_t shm = ((size_t)rows * C + (size_t)ppb * cout2) * sizeof(float);
   HEAD_DISPATCH(cout2, head_out_bwd_apply_kernel, dim3(blocks), dim3(256), shm,
                 as_stream(stream), y, to_act(yd), save, gamma, w2, dout, to_act(doutd), sums,
                 count, ppb, rows, dy, to_act(dyd), ws);
@@ -1158,6 +1345,27 @@ int vae2_conv1x1_upsum_fwd(const float* x, const vae2_act* xd, const float* wp,
   const size_t shm = ((size_t)4 * nu * kUsXB + (size_t)(vtot > 0 ? vtot : 1)) * sizeof(float);
   dim3 grid((unsigned)(yd->n * p.nrb * p.nxb * ncb));
   hipStream_t st = as_stream(stream);
+  bool one = g_upsum_one && yd->w % kUsXB == 0 && p.cin4 <= 20;
+  for (int s = 0; s < nup; ++s)
+    one = one && yd->h == (int64_t)p.zh[s] << (s + 1) && yd->w == (int64_t)p.zw[s] << (s + 1);
+  if (one) {
+#define US2_LAUNCH(N)                                                                   \
+  switch (p.cin4 / 4) {                                                                 \
+    case 1: VAE2_LAUNCH((upsum2_kernel<N, 1>), grid, dim3(256), 0, st, p); break;       \
+    case 2: VAE2_LAUNCH((upsum2_kernel<N, 2>), grid, dim3(256), 0, st, p); break;       \
+    case 3: VAE2_LAUNCH((upsum2_kernel<N, 3>), grid, dim3(256), 0, st, p); break;       \
+    case 4: VAE2_LAUNCH((upsum2_kernel<N, 4>), grid, dim3(256), 0, st, p); break;       \
+    default: VAE2_LAUNCH((upsum2_kernel<N, 5>), grid, dim3(256), 0, st, p); break;      \
+  }
+    switch (nup) {
+      case 0: US2_LAUNCH(0) break;
+      case 1: US2_LAUNCH(1) break;
+      case 2: US2_LAUNCH(2) break;
+      default: US2_LAUNCH(3) break;
+    }
+#undef US2_LAUNCH
+    return check_launch(fn);
+  }
   bool tight = g_upsum_tight != 0;
   for (int s = 0; s < nup; ++s) tight = tight && p.vcols[s] <= 4 * us_vu(s, true);
   const bool kq5 = p.cin4 <= 20;
@@ -1186,10 +1394,11 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
 
 int vae2_heads_set_algo(int algo) {
   const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2) | (g_adj_fused ? 0 : 4) |
-                   (g_adj_band == 32 ? 0 : g_adj_band << 8);
+                   (g_upsum_one ? 0 : 8) | (g_adj_band == 32 ? 0 : g_adj_band << 8);
   g_adj_stream = (algo & 1) ? 0 : 1;
   g_upsum_tight = (algo & 2) ? 0 : 1;
   g_adj_fused = (algo & 4) ? 0 : 1;
+  g_upsum_one = (algo & 8) ? 0 : 1;
   const int band = (algo >> 8) & 0xff;  // one-pass adjoint band rows (0: default 32)
   g_adj_band = band >= 8 && band % 8 == 0 ? band : 32;
   return prev;

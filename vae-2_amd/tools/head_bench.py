@@ -37,7 +37,12 @@ def main():
     ap.add_argument("--h", type=int, default=128)
     ap.add_argument("--w", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma list of upsum,adj,out (profiling runs)")
     a = ap.parse_args()
+    only = set(filter(None, a.only.split(",")))
+
+    def want(k):
+        return not only or k in only
     lib = _lib.load()
     dev = torch.device("cuda")
     split = (18, 36, 72, 144)
@@ -68,11 +73,16 @@ def main():
         call("vae2_conv1x1_upsum_fwd", x0p, ctypes.byref(x0a), ptr(wp0), ptr(bias), 3, ups, upds,
              yp, ctypes.byref(ya), ptr(stats), s)
     zb = sum(z.numel() for z in zs) * 4
-    res.append(("upsum (y write + x0 + z read)", timeit(upsum, a.iters), P * C * 4 + P * 20 * 4 + zb))
-    lib.vae2_heads_set_algo(2)
-    res.append(("  same, 12 staging columns per source", timeit(upsum, a.iters),
-                P * C * 4 + P * 20 * 4 + zb))
-    lib.vae2_heads_set_algo(0)
+    if want("upsum"):
+        res.append(("upsum (y write + x0 + z read)", timeit(upsum, a.iters),
+                    P * C * 4 + P * 20 * 4 + zb))
+        lib.vae2_heads_set_algo(8)
+        res.append(("  LDS-staged kernel (upsum_kernel)", timeit(upsum, a.iters),
+                    P * C * 4 + P * 20 * 4 + zb))
+        lib.vae2_heads_set_algo(8 | 2)
+        res.append(("  same, 12 staging columns per source", timeit(upsum, a.iters),
+                    P * C * 4 + P * 20 * 4 + zb))
+        lib.vae2_heads_set_algo(0)
 
     gs = [new_act((n, h, w_, C), ys[0]) for (h, w_) in sizes[1:]]
     gptrs = (ctypes.c_void_p * 3)(*[act_of(g)[0] for g in gs])
@@ -87,7 +97,7 @@ def main():
     def adj():
         call("vae2_upsample_bilinear_bwd_multi", ynp, ctypes.byref(yna), 3, gptrs, gacts, ptr(uws),
              usz, s)
-    for algo, name in ((0, "upsample adjoint x3, one pass (dy read + dx write)"),
+    for algo, name in () if not want("adj") else ((0, "upsample adjoint x3, one pass (dy read + dx write)"),
                        (16 << 8, "  same, 16 dy rows per workgroup"),
                        (64 << 8, "  same, 64 dy rows per workgroup"),
                        (4, "  two-pass (horizontal -> hb -> vertical)"),
@@ -105,7 +115,8 @@ def main():
     def hfwd():
         call("vae2_head_out_fwd", yp, ctypes.byref(ya), ptr(save), ptr(w2), ptr(b2), 3, op,
              ctypes.byref(oa), s)
-    res.append(("head_out_fwd (y read)", timeit(hfwd, a.iters), P * C * 4))
+    if want("out"):
+        res.append(("head_out_fwd (y read)", timeit(hfwd, a.iters), P * C * 4))
 
     wsz = lib.vae2_head_out_bwd_ws_size(ctypes.byref(ya), 3)
     ws = torch.empty(wsz, device=dev)
@@ -116,7 +127,8 @@ def main():
     def hred():
         call("vae2_head_out_bwd_reduce", yp, ctypes.byref(ya), ptr(save), ptr(w2), 3, op,
              ctypes.byref(oa), ptr(sums), ptr(dg), ptr(db), ptr(dw2), ptr(db2), ptr(ws), wsz, s)
-    res.append(("head_out_bwd_reduce (y read)", timeit(hred, a.iters), P * C * 4))
+    if want("out"):
+        res.append(("head_out_bwd_reduce (y read)", timeit(hred, a.iters), P * C * 4))
     dy = new_act((n, H, W, C), ys[0])
     dyp, dya = act_of(dy)
     yn = new_act((n, H, W, C), ys[0])
@@ -126,11 +138,14 @@ def main():
         call("vae2_head_out_bwd_apply", yp, ctypes.byref(ya), ptr(save), ptr(dg), ptr(w2), 3, op,
              ctypes.byref(oa), ptr(sums), float(P), dyp, ctypes.byref(dya), ptr(dbias), ptr(ws),
              wsz, s)
-    res.append(("head_out_bwd_apply (y read + dy write)", timeit(happ, a.iters), 2 * P * C * 4))
+    if want("out"):
+        res.append(("head_out_bwd_apply (y read + dy write)", timeit(happ, a.iters),
+                    2 * P * C * 4))
 
     def copy():
         dy.copy_(yn)
-    res.append(("torch copy y->dy (reference rate)", timeit(copy, a.iters), 2 * P * C * 4))
+    if want("out"):
+        res.append(("torch copy y->dy (reference rate)", timeit(copy, a.iters), 2 * P * C * 4))
     print(f"shape n={n} {H}x{W}, C={C}")
     for name, us, byts in res:
         print(f"  {name:45s} {us:9.1f} us  {byts / us / 1e3:8.1f} GB/s")
