@@ -157,9 +157,11 @@ __device__ constexpr float hat_w(int d, int f) {
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream);
 
-// Grid size for element-wise kernels: enough blocks to fill 256 CUs several
-// times over, each thread grid-striding.
-inline unsigned ew_blocks(int64_t n, int threads = 256, int64_t cap = 8192) {
+// Grid size for element-wise kernels: one element (or quad) per thread up to 16.7 M of
+// them, then grid-striding.  (A thread that loops stores, then issues its next loads:
+// vmcnt counts stores too, so every iteration after the first also waits for the previous
+// iteration's store -- the 8192-block cap made the 128x256 fuse sums loop 2-3 times.)
+inline unsigned ew_blocks(int64_t n, int threads = 256, int64_t cap = 65536) {
   int64_t b = ceil_div(n, threads);
   if (b > cap) b = cap;
   if (b < 1) b = 1;

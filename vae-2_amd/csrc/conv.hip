@@ -545,7 +545,7 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
       fa[i] = load4(ar, ok ? (uint32_t)(m * p.a_ps + q) * 4u : kOOB);
     }
   };
-  auto step = [&](f4* fa, int st) {
+  auto mma = [&](f4* fa, int st) {
     const int it = st / nch, c = st - it * nch;
     if (cpad && c == nch - 1) {  // channels past a_c in the last quad (a wider buffer's)
       const int q = 16 * c + 4 * g;
@@ -567,6 +567,9 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s2], fb[j][s2], acc[i][j], 0, 0, 0);
+  };
+  auto epi = [&](int st) {
+    const int it = st / nch, c = st - it * nch;
     if (c != nch - 1) return;
     // the tile's epilogue, then a fresh accumulator.  BN partial sums in the MFMA layout
     // (lane = column r, rows 4g..4g+3; statistics only with beta = 0), then each 16x16
@@ -623,14 +626,21 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
       }
     }
   };
+  // Two chunks' loads in flight; a tile's epilogue stores go out after the loads of the
+  // next two chunks (vmcnt counts stores too: a load issued after them would wait for them)
   if (S > 0) {
     f4 fa0[TM], fa1[TM];
     load(fa0, 0);
+    load(fa1, 1);
     for (int st = 0; st < S; st += 2) {
-      load(fa1, st + 1);
-      step(fa0, st);
+      mma(fa0, st);
       load(fa0, st + 2);
-      if (st + 1 < S) step(fa1, st + 1);
+      epi(st);
+      if (st + 1 < S) {
+        mma(fa1, st + 1);
+        load(fa1, st + 3);
+        epi(st + 1);
+      }
     }
   }
   if (p.stats) {

@@ -285,6 +285,17 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
     }
     f4 sdy = {0.f, 0.f, 0.f, 0.f};
     constexpr int U = 2;  // pixels in flight per thread
+    // the next U pixels' y loads go out before this group's dy stores (vmcnt counts
+    // stores too: loads issued after them would wait for them)
+    f4 nv[U];
+    auto ldy = [&](int64_t pb) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = pb + u * rows;
+        nv[u] = p < p1 ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    ldy(p0 + r);
     for (int64_t pb = p0 + r; pb < p1; pb += U * rows) {
       f4 vv[U];
       float dd[U][CO];
@@ -292,10 +303,11 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
       for (int u = 0; u < U; ++u) {
         const int64_t p = pb + u * rows;
         const bool ok = p < p1;
-        vv[u] = ok ? hld4(yb_at(y, P, p, c)) : f4{0.f, 0.f, 0.f, 0.f};
+        vv[u] = nv[u];
 #pragma unroll
         for (int o = 0; o < CO; ++o) dd[u][o] = ok ? sd[(p - p0) * CO + o] : 0.f;
       }
+      if (pb + U * rows < p1) ldy(pb + U * rows);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t p = pb + u * rows;
@@ -561,17 +573,18 @@ template <int S>
 struct Us2Src {
   static constexpr int F = 2 << S, NC = 16 / F + 2;  // source columns px0/F - 1 ... px0/F + 16/F
   float r0[NC], r1[NC];
-  int h0, h1;  // rows held in r0 / r1
+  int h0, h1;      // rows held in r0 / r1
+  float l0, l1;    // vertical weights of the row they serve
 };
 
 template <int S>
 __device__ __forceinline__ void us2_rows(Us2Src<S>& a, const UpSum& p, int n, int oy, int px0,
-                                         int c, bool cok, float& l0, float& l1) {
+                                         int c, bool cok) {
   constexpr int F = Us2Src<S>::F, NC = Us2Src<S>::NC;
   const int num = 2 * oy + 1 - F;
   const int i0 = num >= 0 ? num / (2 * F) : -1;
-  l1 = (float)(num - 2 * F * i0) / (float)(2 * F);
-  l0 = 1.f - l1;
+  a.l1 = (float)(num - 2 * F * i0) / (float)(2 * F);
+  a.l0 = 1.f - a.l1;
   const int zh = p.zh[S], zw = p.zw[S];
   const int ra = i0 < 0 ? 0 : (i0 > zh - 1 ? zh - 1 : i0);
   const int rb = i0 + 1 > zh - 1 ? zh - 1 : i0 + 1;
@@ -599,11 +612,11 @@ __device__ __forceinline__ void us2_rows(Us2Src<S>& a, const UpSum& p, int n, in
 }
 
 template <int S>
-__device__ __forceinline__ void us2_add(const Us2Src<S>& a, float l0, float l1, float* v) {
+__device__ __forceinline__ void us2_add(const Us2Src<S>& a, float* v) {
   constexpr int F = Us2Src<S>::F, NC = Us2Src<S>::NC;
   float vb[NC];
 #pragma unroll
-  for (int q = 0; q < NC; ++q) vb[q] = l0 * a.r0[q] + l1 * a.r1[q];
+  for (int q = 0; q < NC; ++q) vb[q] = a.l0 * a.r0[q] + a.l1 * a.r1[q];
 #pragma unroll
   for (int pp = 0; pp < 16; ++pp) {
     const int o = us2_off(pp, F) + 1;
@@ -646,6 +659,19 @@ __global__ __launch_bounds__(256) void upsum2_kernel(UpSum p) {
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, p.y_bytes);
   const int64_t P = (int64_t)(p.rows / p.nxb / p.nrb) * p.H * p.W;  // n * H * W
   double d1 = 0.0, d2 = 0.0;
+  // Row ry + 1's loads (x0 fragments, source rows that move) are issued before row ry's
+  // stores: vmcnt counts stores too, so a load issued after them would wait for them.
+  float xa[KQ];
+  auto prep = [&](int oy) {
+    const int row = n * p.H + oy;
+    const uint32_t xo = (uint32_t)(((row * p.W + px0 + r) * p.x_ps + g) * 4);
+#pragma unroll
+    for (int kq = 0; kq < KQ; ++kq) xa[kq] = load1(xr, 4 * kq + g < p.cin ? xo + 16u * kq : kOOB);
+    if constexpr (NUP > 0) us2_rows<0>(s0, p, n, oy, px0, c, cok);
+    if constexpr (NUP > 1) us2_rows<1>(s1, p, n, oy, px0, c, cok);
+    if constexpr (NUP > 2) us2_rows<2>(s2, p, n, oy, px0, c, cok);
+  };
+  prep(oy0);
   for (int ry = 0; ry < ny; ++ry) {
     const int oy = oy0 + ry, row = n * p.H + oy;
     float v[16];
@@ -654,14 +680,11 @@ __global__ __launch_bounds__(256) void upsum2_kernel(UpSum p) {
       f4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
-      const uint32_t xo = (uint32_t)(((row * p.W + px0 + r) * p.x_ps + g) * 4);
 #pragma unroll
-      for (int kq = 0; kq < KQ; ++kq) {
-        const float a = load1(xr, 4 * kq + g < p.cin ? xo + 16u * kq : kOOB);
+      for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, fb[kq][j], acc[j], 0, 0, 0);
-      }
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[kq], fb[kq][j], acc[j], 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -669,19 +692,10 @@ __global__ __launch_bounds__(256) void upsum2_kernel(UpSum p) {
 #pragma unroll
       for (int pp = 0; pp < 16; ++pp) v[pp] = xt[pp * 64 + lane];
     }
-    float l0, l1;
-    if constexpr (NUP > 0) {
-      us2_rows<0>(s0, p, n, oy, px0, c, cok, l0, l1);
-      us2_add<0>(s0, l0, l1, v);
-    }
-    if constexpr (NUP > 1) {
-      us2_rows<1>(s1, p, n, oy, px0, c, cok, l0, l1);
-      us2_add<1>(s1, l0, l1, v);
-    }
-    if constexpr (NUP > 2) {
-      us2_rows<2>(s2, p, n, oy, px0, c, cok, l0, l1);
-      us2_add<2>(s2, l0, l1, v);
-    }
+    if constexpr (NUP > 0) us2_add<0>(s0, v);
+    if constexpr (NUP > 1) us2_add<1>(s1, v);
+    if constexpr (NUP > 2) us2_add<2>(s2, v);
+    if (ry + 1 < ny) prep(oy + 1);
     const uint32_t ybase = (uint32_t)(cbi * P * 64 + ((int64_t)row * p.W + px0) * 64 + lane);
     float q1 = 0.f, q2 = 0.f;
 #pragma unroll
