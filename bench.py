@@ -253,7 +253,8 @@ def main():
     for kv in filter(None, args.conv_tune.split(",")):
         from vae2 import _lib
         k, v = kv.split("=")
-        _lib.load().vae2_conv2d_set_tune(int(k), int(v))
+        if _lib.load().vae2_conv2d_set_tune(int(k), int(v)) < 0:
+            raise SystemExit(f"unknown conv tune key {k}")
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False

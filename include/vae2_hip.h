@@ -76,8 +76,9 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * columns take 2 x 16 output-channel rows and all 64 columns per workgroup (not 4 x 16
  * rows and 48 + 48 columns); key 2 = 1: the direct 3x3 kernels' 8-row tiles run as 8
  * waves of one row each (512 threads) instead of 4 waves of two rows; key 3 = 1: the
- * 18 / 36 / 72-channel 3x3 weight gradients spread their column tiles over 8 waves.
- * Returns the previous value, -1 for an unknown key.                                    */
+ * 18 / 36 / 72-channel 3x3 weight gradients spread their column tiles over 8 waves;
+ * key 4 = the persistent 1x1 GEMM's maximum N tiles (of 16 channels) per workgroup, 3..8
+ * (default 4).  Returns the previous value, -1 for an unknown key.                      */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab

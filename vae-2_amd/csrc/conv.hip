@@ -1210,9 +1210,15 @@ int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink 
 int g_wgrad_cols = 1;     // vae2_conv2d_set_tune key 1: weight-gradient column blocks (pick_wtile)
 int g_dconv_nw8 = 0;      // vae2_conv2d_set_tune key 2: direct 3x3 8-row tiles as 8 waves
 int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients over 8 waves
+// key 4: the 1x1 GEMM's N tiles per workgroup (3..8).  4 by default: the TN = 8 instance
+// holds 264 VGPRs (1 wave / SIMD) and its persistent grid was sized for 3 per CU, i.e. ran in
+// 3 rounds; with the grid from the occupancy query, conv_bench 64->256 forward 172 (TN 8,
+// LDS-sized grid) -> 157 (TN 8) -> 131 us (TN 4, 152 VGPRs), 256->64 data gradient
+// 153 -> 127 us; step 845.1 / 845.4 (8) vs 847.3 / 848.0 frames/s (4), same box.
+int g_gemm1_tn = 4;
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8;
+    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1267,6 +1273,7 @@ struct G1Tile {
   int tn, nblk, grid_x;
   size_t lds;
 };
+int gemm1_blocks_per_cu(int tn, size_t lds);
 
 static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
                        const float* a, G1Tile* out) {
@@ -1278,12 +1285,16 @@ static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride
   const int k4 = round_up((int)ad->c, 4);
   const int tiles = (N + 15) / 16;
   G1Tile t;
-  t.nblk = (tiles + 7) / 8;
+  const int tn_max = g_gemm1_tn >= 3 && g_gemm1_tn <= 8 ? g_gemm1_tn : 4;
+  t.nblk = (tiles + tn_max - 1) / tn_max;
   t.tn = (tiles + t.nblk - 1) / t.nblk;
+  if (t.tn < 3) t.tn = 3;
   const int nch = (k4 + 15) / 16;
   t.lds = (size_t)16 * t.tn * (nch * 16 + 4) * sizeof(float);
   if (t.lds > 96 * 1024) return false;
-  const int per_cu = t.lds <= 40 * 1024 ? 3 : (t.lds <= 64 * 1024 ? 2 : 1);
+  // resident workgroups per CU (registers and LDS; the TN = 8 instance holds 264 VGPRs:
+  // one wave per SIMD) -- the persistent grid is exactly that many per CU
+  const int per_cu = gemm1_blocks_per_cu(t.tn, t.lds);
   const int64_t ntiles = ceil_div(M, 32);
   int64_t gx = 256 * per_cu / t.nblk;
   if (gx > ceil_div(ntiles, 4)) gx = ceil_div(ntiles, 4);
@@ -2065,6 +2076,38 @@ static uint32_t act_bytes(const vae2_act* d) {
 }
 
 #if VAE2_PART(1)
+// hipOccupancyMaxActiveBlocksPerMultiprocessor of gemm1x1_kernel<2, tn> with `lds` bytes
+// of dynamic LDS (cached per (tn, lds)); at least 1.
+int gemm1_blocks_per_cu(int tn, size_t lds) {
+  static int cache[9][4] = {};
+  static size_t cache_lds[9][4] = {};
+  if (tn < 3 || tn > 8) return 1;
+  for (int i = 0; i < 4; ++i)
+    if (cache[tn][i] && cache_lds[tn][i] == lds) return cache[tn][i];
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (tn) {
+#define CASE(T)                                                                          \
+  case T:                                                                                \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(                                    \
+        &n, reinterpret_cast<const void*>(gemm1x1_kernel<2, T>), 256, lds);              \
+    break;
+    CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+  }
+  if (e != hipSuccess || n < 1) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  for (int i = 0; i < 4; ++i)
+    if (!cache[tn][i]) {
+      cache[tn][i] = n;
+      cache_lds[tn][i] = lds;
+      break;
+    }
+  return n;
+}
+
 int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
                  const G1Tile& t, hipStream_t s, const char* fn) {
@@ -2460,7 +2503,8 @@ int vae2_conv2d_pack_weights(const vae2_pack_job* jobs, int64_t njobs, void* str
 }
 
 // Launch-shape tuning knobs (A/B measurements; every setting computes the same result):
-// key 0 = igemm minimum workgroups (0: the default row-tile rule).  Returns the previous
+// key 0 = igemm minimum workgroups (0: the default row-tile rule); key 4 = gemm1x1 N tiles
+// per workgroup (3..8).  Returns the previous
 // value, or -1 for an unknown key.
 int vae2_conv2d_set_tune(int key, int value) {
   if (key == 0) {
@@ -2481,6 +2525,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 3) {
     const int prev = g_wgrad_nw8;
     g_wgrad_nw8 = value ? 1 : 0;
+    return prev;
+  }
+  if (key == 4) {
+    const int prev = g_gemm1_tn;
+    g_gemm1_tn = value >= 3 && value <= 8 ? value : 4;
     return prev;
   }
   return -1;

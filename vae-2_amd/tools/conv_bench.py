@@ -83,7 +83,8 @@ def main():
     torch.cuda.synchronize()
     for kv in filter(None, a.tune.split(",")):
         k, v = kv.split("=")
-        lib.vae2_conv2d_set_tune(int(k), int(v))
+        if lib.vae2_conv2d_set_tune(int(k), int(v)) < 0:
+            raise SystemExit(f"unknown conv tune key {k}")
     for algo in a.algo:
         lib.vae2_conv2d_set_algo(algo)
         lib.vae2_conv2d_set_mfma_bf16(1 if a.bf16 else 0)
