@@ -12,6 +12,7 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${TAG}_p
   python bench.py --no-cpu-baseline --profile-json gpurun_out/${TAG}_profile_rp.json \
   > gpurun_out/${TAG}_bench_rp.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_rp.log; exit 1; }
 CSV=$(find gpurun_out/${TAG}_prof -name '*kernel_trace.csv' | head -1)
-python vae-2_amd/tools/trace_steps.py "$CSV" --steps 10 --json gpurun_out/${TAG}_steps.json \
+# the 8 last graph-replayed timed steps (bench.py's 3 eager roofline steps come after them)
+python vae-2_amd/tools/trace_steps.py "$CSV" --steps 8 --skip 3 --json gpurun_out/${TAG}_steps.json \
   > gpurun_out/${TAG}_steps.txt 2>&1
 head -40 gpurun_out/${TAG}_steps.txt

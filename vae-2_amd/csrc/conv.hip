@@ -2339,6 +2339,11 @@ struct W3Tile {
   int nw = 4;  // waves per workgroup (wgrad3_kernel NW)
 };
 
+// Resident workgroups per CU of the wgrad3_kernel instance a tile selects (PART(3): the
+// launch dispatch run in probe mode + hipOccupancyMaxActiveBlocksPerMultiprocessor).
+int wgrad3_blocks_per_cu(const W3Tile& t, size_t lds);
+static size_t wgrad3_lds(const W3Tile& t);
+
 static bool wgrad3_shape_ok(const vae2_act* xd, const vae2_act* dyd, int k, int stride, int pad) {
   // (the KS = 1 form of the kernel measured slower than the gather kernel on 1x1 convs:
   //  without the 9-tap reuse the staging does not pay for itself)
@@ -2389,9 +2394,10 @@ static W3Tile pick_w3tile(const vae2_act* xd, const vae2_act* dyd, int k) {
   t.tps = (int)ceil_div(t.ntiles, want);
   t.pf = (int64_t)t.ntiles * gy >= 1024;
   if (t.pf) {
-    // one wave of workgroups: the prefetching variants hold 1 (TM >= 3) or 2
-    // workgroups per CU, so use exactly that many in all (no straggler wave)
-    const int64_t resident = t.tm >= 3 ? 256 : 512;
+    // one wave of workgroups: exactly as many as are resident at once (no straggler wave);
+    // the residency comes from the instance's registers / LDS (the 18-channel 8-wave form
+    // holds 145 VGPRs: one 512-thread workgroup per CU, not the 2 assumed before)
+    const int64_t resident = 256 * (int64_t)wgrad3_blocks_per_cu(t, wgrad3_lds(t));
     int64_t w2 = resident / gy > 0 ? resident / gy : 1;
     if (w2 * slab > cap) w2 = cap / slab > 0 ? cap / slab : 1;
     t.tps = (int)ceil_div(t.ntiles, w2);
@@ -2413,20 +2419,38 @@ static size_t wgrad3_lds(const W3Tile& t) {
 }
 
 #if VAE2_PART(3)
+// Probe mode of the wgrad3 dispatch: record the instance (and its block size) instead of
+// launching it.
+struct W3Probe {
+  bool on = false;
+  const void* fn = nullptr;
+  unsigned threads = 0;
+};
+static thread_local W3Probe g_w3probe;
+#define W3_LAUNCH(K, GRID, BLOCK, SHM, S, ...)                         \
+  do {                                                                \
+    if (g_w3probe.on) {                                               \
+      g_w3probe.fn = reinterpret_cast<const void*>(K);                \
+      g_w3probe.threads = dim3(BLOCK).x;                              \
+    } else {                                                          \
+      VAE2_LAUNCH(K, GRID, BLOCK, SHM, S, __VA_ARGS__);               \
+    }                                                                 \
+  } while (0)
+
 template <int TM, int BH, bool PF>
 static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t shm,
                              hipStream_t s, int nr = 0, int nw = 4) {
   if constexpr (TM == 1 || TM == 2) {
     if (nr && nw == 8) {  // 8 waves: (TM, TN) = (1, 2) or (2, 3) (pick_w3tile)
       constexpr int R = TM == 1 ? 2 : 4, T8 = TM == 1 ? 2 : 3;
-      VAE2_LAUNCH((wgrad3_kernel<TM, T8, BH, PF, 3, false, R, 8>), grid, dim3(512), shm, s, p);
+      W3_LAUNCH((wgrad3_kernel<TM, T8, BH, PF, 3, false, R, 8>), grid, dim3(512), shm, s, p);
       return;
     }
     if (nr) {  // (TM, NR) = (1, 2) or (2, 4): pick_w3tile, fp32 operands
       constexpr int R = TM == 1 ? 2 : 4;
       switch (tn) {
 #define CASE(T) \
-  case T: VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, false, R>), grid, dim3(256), shm, s, p); break;
+  case T: W3_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, false, R>), grid, dim3(256), shm, s, p); break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
 #undef CASE
       }
@@ -2434,15 +2458,15 @@ static void wgrad3_launch_tn(const WGrad3& p, int tn, int ks, dim3 grid, size_t 
     }
   }
   if (ks == 1) {  // 1x1: at most 64 channels = 4 column tiles per slab, one per wave
-    if (g_bf16) VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1, true>), grid, dim3(256), shm, s, p);
-    else VAE2_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
+    if (g_bf16) W3_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1, true>), grid, dim3(256), shm, s, p);
+    else W3_LAUNCH((wgrad3_kernel<TM, 1, BH, PF, 1>), grid, dim3(256), shm, s, p);
     return;
   }
   switch (tn) {
 #define CASE(T) \
   case T:                                                                         \
-    if (g_bf16) VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, true>), grid, dim3(256), shm, s, p); \
-    else VAE2_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p);   \
+    if (g_bf16) W3_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3, true>), grid, dim3(256), shm, s, p); \
+    else W3_LAUNCH((wgrad3_kernel<TM, T, BH, PF, 3>), grid, dim3(256), shm, s, p);   \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6)
 #undef CASE
@@ -2465,6 +2489,38 @@ static void wgrad3_launch(const WGrad3& p, const W3Tile& t, dim3 grid, size_t sh
                           hipStream_t s) {
   if (t.pf) wgrad3_launch_tm<BH, true>(p, t, grid, shm, s);
   else wgrad3_launch_tm<BH, false>(p, t, grid, shm, s);
+}
+
+int wgrad3_blocks_per_cu(const W3Tile& t, size_t lds) {
+  struct Key {
+    int tm, tn, bh, ks, nr, nw, pf, bf;
+    size_t lds;
+    int n;
+  };
+  static Key cache[32];
+  static int ncache = 0;
+  const int bf = g_bf16;
+  for (int i = 0; i < ncache; ++i) {
+    const Key& k = cache[i];
+    if (k.tm == t.tm && k.tn == t.tn && k.bh == t.bh && k.ks == t.ks && k.nr == t.nr &&
+        k.nw == t.nw && k.pf == (int)t.pf && k.bf == bf && k.lds == lds)
+      return k.n;
+  }
+  WGrad3 p{};
+  g_w3probe = W3Probe{};
+  g_w3probe.on = true;
+  if (t.bh == 8) wgrad3_launch<8>(p, t, dim3(1), lds, nullptr);
+  else wgrad3_launch<4>(p, t, dim3(1), lds, nullptr);
+  g_w3probe.on = false;
+  int n = 0;
+  if (!g_w3probe.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &n, g_w3probe.fn, (int)g_w3probe.threads, lds) != hipSuccess ||
+      n < 1) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  if (ncache < 32) cache[ncache++] = Key{t.tm, t.tn, t.bh, t.ks, t.nr, t.nw, (int)t.pf, bf, lds, n};
+  return n;
 }
 #endif  // VAE2_PART(3)
 

@@ -40,7 +40,7 @@ def load(path):
     with open(path) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
-                         kernel_name(r["Kernel_Name"])))
+                         kernel_name(r["Kernel_Name"]), int(r.get("Queue_Id") or 0)))
     rows.sort()
     return rows
 
@@ -62,7 +62,7 @@ def select_steps(rows, steps, marker="adam", skip=0):
 
 def busy_ns(sel):
     busy, cur_s, cur_e = 0, None, None
-    for s, e, _ in sel:
+    for s, e, *_ in sel:
         if cur_e is None or s > cur_e:
             if cur_e is not None:
                 busy += cur_e - cur_s
@@ -74,7 +74,7 @@ def busy_ns(sel):
 
 def breakdown(sel, k):
     fam, ker, inst = (defaultdict(lambda: [0, 0]) for _ in range(3))
-    for s, e, n in sel:
+    for s, e, n, *_ in sel:
         for d, key in ((fam, family(n)), (ker, short(n)), (inst, n)):
             d[key][0] += e - s
             d[key][1] += 1
@@ -85,7 +85,13 @@ def breakdown(sel, k):
         return [{"name": n, "ms_per_step": t / k / 1e6, "launches_per_step": c / k,
                  "avg_us": t / c / 1e3} for n, (t, c) in sorted(d.items(), key=lambda x: -x[1][0])]
 
-    return {"steps": k, "wall_ms_per_step": (t1 - t0) / k / 1e6,
+    queues = defaultdict(list)
+    for r in sel:
+        queues[r[3] if len(r) > 3 else 0].append(r)
+    qt = [{"queue": q, "busy_ms_per_step": busy_ns(v) / k / 1e6,
+           "kernel_ms_per_step": sum(e - s for s, e, *_ in v) / k / 1e6,
+           "launches_per_step": len(v) / k} for q, v in sorted(queues.items())]
+    return {"steps": k, "wall_ms_per_step": (t1 - t0) / k / 1e6, "queues": qt,
             "busy_ms_per_step": busy_ns(sel) / k / 1e6, "kernel_ms_per_step": total / k / 1e6,
             "launches_per_step": len(sel) / k, "families": table(fam), "kernels": table(ker),
             "instances": table(inst)}
@@ -106,6 +112,10 @@ def main():
     print(f"steps {b['steps']}: wall/step {b['wall_ms_per_step']:.2f} ms, busy/step "
           f"{b['busy_ms_per_step']:.2f} ms, summed kernel/step {b['kernel_ms_per_step']:.2f} ms, "
           f"launches/step {b['launches_per_step']:.0f}")
+    print("-- hardware queues (HIP streams): busy = union of the queue's kernel intervals")
+    for q in b["queues"]:
+        print(f"  queue {q['queue']:3d}  busy {q['busy_ms_per_step']:7.2f} ms  kernels "
+              f"{q['kernel_ms_per_step']:7.2f} ms  {q['launches_per_step']:7.1f} launches")
     for title, key, lim in (("families", "families", None), ("kernels", "kernels", None),
                             ("top instances", "instances", a.instances)):
         print(f"-- {title}")
