@@ -438,7 +438,9 @@ int vae2_fuse_sum_relu_bn(int n, const float* const* xs, const vae2_act* xds,
  * the power-of-two upsampling adjoint instead of the row-streaming one; bit 1 = the
  * up-sum kernel with 12 staging columns for every source (instead of 12 / 6 / 3 for
  * halving source resolutions); bit 2 = the two-pass (horizontal, then vertical through a
- * workspace) power-of-two adjoint instead of the one-pass band kernel; bits 8-15 = the
+ * workspace) power-of-two adjoint instead of the one-pass band kernel; bit 3 = the
+ * LDS-staged up-sum instead of the one-pass kernel; bits 4 / 5 = 4 instead of 2 pixels in
+ * flight per thread in the head backward reduce / apply passes; bits 8-15 = the
  * one-pass kernel's dy rows per workgroup (a multiple of 8; 0 = 32).  Returns the
  * previous setting.  Process-wide.                                                    */
 int vae2_heads_set_algo(int algo);

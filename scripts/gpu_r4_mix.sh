@@ -7,7 +7,8 @@ TAG=${1:-mx}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest --maxfail=3 -q --timeout 300 --timeout-method thread \
-  tests/test_heads_gpu.py tests/test_kernels_gpu.py tests/test_bench_instances_gpu.py -m gpu \
+  tests/test_heads_gpu.py tests/test_kernels_gpu.py tests/test_bench_instances_gpu.py \
+  tests/test_lazy_bn_gpu.py -m gpu \
   > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_tests.log
 [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/${TAG}_tests.log | head -30; exit $rc; }

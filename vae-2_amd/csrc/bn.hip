@@ -298,17 +298,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q_kernel(
 // ... of column c; with `two`, also of the second block of rows): 4 rows' loads issued
 // before their adds (latency, not bandwidth, bounds these small reductions), the adds
 // in the same order as a plain strided loop, so the result is bit for bit the same.
+// Range-checked buffer loads (rows past the end load 0): with `r < rows ? part[..] : 0`
+// hipcc branched around each load and waited for it (16 dependent round trips per pass).
 __device__ __forceinline__ void rows_sum2(const float* __restrict__ part, int64_t rows,
                                           int64_t C, int c, int tid, double& a, double& b,
                                           bool two = true) {
   constexpr int U = 8;
+  const int64_t nb = (two ? 2 : 1) * rows * C * 4;
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, (uint32_t)(nb < (int64_t)kOOB ? nb : kOOB));
   for (int64_t r0 = tid; r0 < rows; r0 += 256 * U) {
     float x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t r = r0 + 256 * u;
-      x[u] = r < rows ? part[r * C + c] : 0.f;
-      y[u] = (two && r < rows) ? part[(rows + r) * C + c] : 0.f;
+      x[u] = load1(pr, r < rows ? (uint32_t)((r * C + c) * 4) : kOOB);
+      y[u] = load1(pr, two && r < rows ? (uint32_t)(((rows + r) * C + c) * 4) : kOOB);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

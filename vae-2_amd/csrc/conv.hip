@@ -704,6 +704,7 @@ struct DConv {
   const float* bx;
   int bx_ps, brelu;
   const float* bsave;
+  uint32_t bx_bytes;  // bx extent for the range-checked epilogue loads
   int vec_out;  // y 16-byte aligned, y_ps % 4 == 0, no statistics with beta != 0
 };
 
@@ -981,7 +982,38 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int oh = oh0 + wave * (TM / 2) + (i >> 1);
-      if (p.stats) {
+      if (p.stats && bnp) {
+        // the row tile's 4 x TN pre-BN values in one batch of range-checked loads (one
+        // round trip; loads guarded by branches waited on each element in turn)
+        const __amdgpu_buffer_rsrc_t bxr = make_rsrc(p.bx, p.bx_bytes);
+        float xv[4][TN];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
+          const bool pin = oh < p.img_h && ow < p.img_w;
+          const int64_t pix = pin ? (int64_t)(img_base + oh) * p.img_w + ow : 0;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            xv[e][j] = load1(bxr, pin && n < p.n ? (uint32_t)((pix * p.bx_ps + n) * 4) : kOOB);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
+          const bool pin = oh < p.img_h && ow < p.img_w;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            const float v = acc[i][j][e] + (p.bias && n < p.n ? p.bias[n] : 0.f);
+            const float x = xv[e][j];
+            const float gv = (p.brelu && !(__builtin_fmaf(x, bsc[j], bsh[j]) > 0.f)) ? 0.f : v;
+            const bool ok = pin && n < p.n;
+            csum[j] += ok ? gv : 0.f;
+            csq[j] += ok ? gv * (x - bmn[j]) * bis[j] : 0.f;
+          }
+        }
+      } else if (p.stats) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int ow = ow0 + (i & 1) * 16 + g * 4 + e;
@@ -1076,6 +1108,17 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
       rsq[j] = 0.f;
       if ((j & 3) != g) continue;
       const int n = n0 + BN + j;
+      float bxv[TM];  // the pre-BN values of the TM pixels, one batch of loads (bnp)
+      if (bnp) {
+        const __amdgpu_buffer_rsrc_t bxr = make_rsrc(p.bx, p.bx_bytes);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int oh = oh0 + wave * (TM / 2) + (i >> 1), ow = ow0 + (i & 1) * 16 + r;
+          const bool in = oh < p.img_h && ow < p.img_w;
+          const int64_t pix = (int64_t)(img_base + (in ? oh : 0)) * p.img_w + (in ? ow : 0);
+          bxv[i] = load1(bxr, in ? (uint32_t)((pix * p.bx_ps + n) * 4) : kOOB);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int oh = oh0 + wave * (TM / 2) + (i >> 1), ow = ow0 + (i & 1) * 16 + r;
@@ -1087,7 +1130,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         if (p.beta != 0.f && in) v += p.beta * *yp;
         if (in && (!(VAE2_ABLATE & 2) || v == 1234.5f)) *yp = v;
         if (bnp) {
-          const float xv = in ? p.bx[pix * p.bx_ps + n] : 0.f;
+          const float xv = bxv[i];
           const float gv = (p.brelu && !(__builtin_fmaf(xv, p.bsave[2 * p.n + n],
                                                         p.bsave[3 * p.n + n]) > 0.f)) ? 0.f : v;
           rsum[j] += in ? gv : 0.f;
@@ -2215,6 +2258,7 @@ struct BnSide {
   const float* bx = nullptr;
   int bx_ps = 0, brelu = 0;
   const float* bsave = nullptr;
+  uint32_t bx_bytes = 0;
 };
 
 int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
@@ -2308,6 +2352,7 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.stats = stats;
   p.isave = bn.isave; p.irelu = bn.irelu;
   p.bx = bn.bx; p.bx_ps = bn.bx_ps; p.brelu = bn.brelu; p.bsave = bn.bsave;
+  p.bx_bytes = bn.bx_bytes;
   p.vec_out = g_vec_out && vec_ok(y, (int)yd->ps) && !(stats && beta != 0.f);
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
   const size_t shm = dconv_shm(d);
@@ -2794,6 +2839,7 @@ int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const floa
   BnSide bn;
   bn.bx = bn_x;
   bn.bx_ps = (int)bn_xd->ps;
+  bn.bx_bytes = act_bytes(bn_xd);
   bn.bsave = bn_save;
   bn.brelu = relu ? 1 : 0;
   return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),

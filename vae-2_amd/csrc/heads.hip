@@ -130,7 +130,7 @@ __device__ __forceinline__ HeadCoef head_coef(const float* save, int c, int C) {
 }
 
 // Partial-row columns: [0,C) sum g | [C,2C) sum g*xhat | [2C, 2C+CO*C) dW2[o][c] | CO x db2
-template <int CO>
+template <int CO, int U = 2>
 __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
     const float* __restrict__ y, Act yd, const float* __restrict__ save,
     const float* __restrict__ w2, const float* __restrict__ dout, Act dod, int64_t ppb,
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_reduce_kernel(
     float db[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) { dw[o] = s0; db[o] = 0.f; }
-    constexpr int U = 2;  // pixels in flight per thread (4 waves/SIMD: 120 -> 95 us per head; 1 and 4 slower)
+    // U pixels in flight per thread (2: 4 waves/SIMD, 120 -> 95 us per head in round 2)
     for (int64_t pb = p0 + r; pb < p1; pb += U * rows) {
       f4 vv[U];
       float dd[U][CO];
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(1024) void head_bwd_colsum_kernel(
 
 // dy = gamma*invstd*(g - sum_g/count - xhat*sum_gxhat/count); partial rows [block][C]
 // of sum_p dy (the wide conv's bias gradient).
-template <int CO>
+template <int CO, int U = 2>
 __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
     const float* __restrict__ y, Act yd, const float* __restrict__ save,
     const float* __restrict__ gamma, const float* __restrict__ w2,
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void head_out_bwd_apply_kernel(
       k4[k] = (gamma ? gamma[ch] : 1.f) * hc.invstd[k];
     }
     f4 sdy = {0.f, 0.f, 0.f, 0.f};
-    constexpr int U = 2;  // pixels in flight per thread
+    // U pixels in flight per thread
     // the next U pixels' y loads go out before this group's dy stores (vmcnt counts
     // stores too: loads issued after them would wait for them)
     f4 nv[U];
@@ -1005,6 +1005,8 @@ __global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
 static int g_adj_stream = 1;  // vae2_heads_set_algo bit 0 clears it
 static int g_upsum_tight = 1;  // vae2_heads_set_algo bit 1 clears it
 static int g_upsum_one = 1;    // vae2_heads_set_algo bit 3 clears it (upsum2_kernel)
+static int g_head_red_u = 2;   // vae2_heads_set_algo bit 4: 4 pixels in flight (backward reduce)
+static int g_head_app_u = 2;   // vae2_heads_set_algo bit 5: 4 pixels in flight (backward apply)
 
 template <int S>
 __global__ __launch_bounds__(256) void up_adj2_vs_kernel(UpAdj p, FastDiv cdiv) {
@@ -1225,6 +1227,18 @@ static bool head_args_ok(const float* y, const vae2_act* yd, int cout2) {
     case 3: VAE2_LAUNCH((KERNEL<3>), __VA_ARGS__); break;          \
     default: VAE2_LAUNCH((KERNEL<4>), __VA_ARGS__); break;         \
   }
+// with U pixels in flight per thread (2 or 4)
+#define HEAD_DISPATCH_U(CO_, U_, KERNEL, ...)                                  \
+  if ((U_) == 4) {                                                             \
+    switch (CO_) {                                                             \
+      case 1: VAE2_LAUNCH((KERNEL<1, 4>), __VA_ARGS__); break;                 \
+      case 2: VAE2_LAUNCH((KERNEL<2, 4>), __VA_ARGS__); break;                 \
+      case 3: VAE2_LAUNCH((KERNEL<3, 4>), __VA_ARGS__); break;                 \
+      default: VAE2_LAUNCH((KERNEL<4, 4>), __VA_ARGS__); break;                \
+    }                                                                          \
+  } else {                                                                     \
+    HEAD_DISPATCH(CO_, KERNEL, __VA_ARGS__)                                    \
+  }
 
 }  // namespace vae2
 
@@ -1273,7 +1287,7 @@ int vae2_head_out_bwd_reduce(const float* y, const vae2_act* yd, const float* sa
   const unsigned blocks = (unsigned)ceil_div(P, ppb);
   const size_t shm = ((size_t)rows * NC + (size_t)ppb * cout2) * sizeof(float);
   VAE2_REQUIRE(shm <= 64 * 1024, fn, "too many channels for the LDS reduction");
-  HEAD_DISPATCH(cout2, head_out_bwd_reduce_kernel, dim3(blocks), dim3(256), shm,
+  HEAD_DISPATCH_U(cout2, g_head_red_u, head_out_bwd_reduce_kernel, dim3(blocks), dim3(256), shm,
                 as_stream(stream), y, to_act(yd), save, w2, dout, to_act(doutd), ppb, rows, ws);
   int rc = check_launch(fn);
   if (rc) return rc;
@@ -1300,7 +1314,7 @@ int vae2_head_out_bwd_apply(const float* y, const vae2_act* yd, const float* sav
   const int64_t P = act_pixels(yd), ppb = head_ppb(P, 1024);
   const unsigned blocks = (unsigned)ceil_div(P, ppb);
   const size_t shm = ((size_t)rows * C + (size_t)ppb * cout2) * sizeof(float);
-  HEAD_DISPATCH(cout2, head_out_bwd_apply_kernel, dim3(blocks), dim3(256), shm,
+  HEAD_DISPATCH_U(cout2, g_head_app_u, head_out_bwd_apply_kernel, dim3(blocks), dim3(256), shm,
                 as_stream(stream), y, to_act(yd), save, gamma, w2, dout, to_act(doutd), sums,
                 count, ppb, rows, dy, to_act(dyd), ws);
   int rc = check_launch(fn);
@@ -1408,11 +1422,14 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
 
 int vae2_heads_set_algo(int algo) {
   const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2) | (g_adj_fused ? 0 : 4) |
-                   (g_upsum_one ? 0 : 8) | (g_adj_band == 32 ? 0 : g_adj_band << 8);
+                   (g_upsum_one ? 0 : 8) | (g_head_red_u == 4 ? 16 : 0) |
+                   (g_head_app_u == 4 ? 32 : 0) | (g_adj_band == 32 ? 0 : g_adj_band << 8);
   g_adj_stream = (algo & 1) ? 0 : 1;
   g_upsum_tight = (algo & 2) ? 0 : 1;
   g_adj_fused = (algo & 4) ? 0 : 1;
   g_upsum_one = (algo & 8) ? 0 : 1;
+  g_head_red_u = (algo & 16) ? 4 : 2;
+  g_head_app_u = (algo & 32) ? 4 : 2;
   const int band = (algo >> 8) & 0xff;  // one-pass adjoint band rows (0: default 32)
   g_adj_band = band >= 8 && band % 8 == 0 ? band : 32;
   return prev;

@@ -242,15 +242,24 @@ struct UpAdjQ {
 };
 
 // sum_d hat_w(d, F) v[F*i + d] over a line of `len` points with stride `st`, edges folded.
+// Every tap's load is unconditional (out-of-line taps read a clamped in-line point with
+// weight 0): guarded loads were branched around one by one, each waited for in turn.
 template <int F>
 __device__ __forceinline__ f4v hat_adj(const float* line, int64_t st, int len, int i, int n_src) {
   constexpr int HF = F / 2;
   const int x0 = F * i;
+  f4v v[4 * HF];
+#pragma unroll
+  for (int d = -HF; d < 3 * HF; ++d) {
+    const int x = x0 + d;
+    const int xc = x < 0 ? 0 : (x >= len ? len - 1 : x);
+    v[d + HF] = *reinterpret_cast<const f4v*>(line + xc * st);
+  }
   f4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int d = -HF; d < 3 * HF; ++d) {
     const int x = x0 + d;
-    if (x >= 0 && x < len) acc += hat_w(d, F) * *reinterpret_cast<const f4v*>(line + x * st);
+    if (x >= 0 && x < len) acc += hat_w(d, F) * v[d + HF];
   }
   if (i == 0) {  // virtual source -1: points d - F
 #pragma unroll
@@ -703,7 +712,9 @@ static int fuse_sum_relu_impl(int n, const float* const* xs, const vae2_act* xds
   }
   int64_t total = act_elems(yd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
-  VAE2_LAUNCH(fuse_sum_relu_kernel, dim3(ew_blocks(total)), dim3(256), 0,
+  // (grid-striding over 8192 blocks: one element per thread measured 27 -> 33 us per
+  // launch in the step trace -- the per-thread index setup is amortised over 2-3 elements)
+  VAE2_LAUNCH(fuse_sum_relu_kernel, dim3(ew_blocks(total, 256, 8192)), dim3(256), 0,
                      as_stream(stream), t, y, to_act(yd), FastDiv((uint32_t)yd->c),
                      FastDiv((uint32_t)yd->w), FastDiv((uint32_t)yd->h));
   return check_launch(fn);

@@ -129,6 +129,9 @@ def main():
              ctypes.byref(oa), ptr(sums), ptr(dg), ptr(db), ptr(dw2), ptr(db2), ptr(ws), wsz, s)
     if want("out"):
         res.append(("head_out_bwd_reduce (y read)", timeit(hred, a.iters), P * C * 4))
+        lib.vae2_heads_set_algo(16)
+        res.append(("  same, 4 pixels in flight per thread", timeit(hred, a.iters), P * C * 4))
+        lib.vae2_heads_set_algo(0)
     dy = new_act((n, H, W, C), ys[0])
     dyp, dya = act_of(dy)
     yn = new_act((n, H, W, C), ys[0])
@@ -141,6 +144,10 @@ def main():
     if want("out"):
         res.append(("head_out_bwd_apply (y read + dy write)", timeit(happ, a.iters),
                     2 * P * C * 4))
+        lib.vae2_heads_set_algo(32)
+        res.append(("  same, 4 pixels in flight per thread", timeit(happ, a.iters),
+                    2 * P * C * 4))
+        lib.vae2_heads_set_algo(0)
 
     def copy():
         dy.copy_(yn)
