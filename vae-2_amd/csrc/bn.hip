@@ -100,10 +100,14 @@ __global__ __launch_bounds__(256) void chan_partials_kernel(
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
+// Per-channel coefficients of a channel quad: unconditional loads of clamped channels (a
+// guarded load is branched around and waited for on its own), zero past C.
 __device__ __forceinline__ f4 chan4(const float* a, int c, int C) {
   f4 v;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] = (c + k < C) ? a[c + k] : 0.f;
+  for (int k = 0; k < 4; ++k) v[k] = a[c + k < C ? c + k : C - 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = c + k < C ? v[k] : 0.f;
   return v;
 }
 
@@ -609,14 +613,25 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
   f4 rsc = {0.f, 0.f, 0.f, 0.f}, rsh = rsc;
   if (L.rx) { rsc = chan4(L.rsave + 2 * C, c, C); rsh = chan4(L.rsave + 3 * C, c, C); }
   const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  // every load unconditional (pixels past P re-read pixel P-1, never stored) and the
+  // uniform branches outside the pixel loop, so the loads of all pixels go out together
   f4 v[kApplyU], rv[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
-    const int64_t p = pb + u * L.rows;
-    if (p < L.P) {
-      v[u] = ld4(L.x + p * L.x_ps + c);
-      if (L.a) rv[u] = ld4(L.a + p * L.a_ps + c);
-      else if (L.rx) rv[u] = ld4(L.rx + p * L.rx_ps + c);
+    const int64_t p = pb + u * L.rows < L.P ? pb + u * L.rows : L.P - 1;
+    v[u] = ld4(L.x + p * L.x_ps + c);
+  }
+  if (L.a) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      const int64_t p = pb + u * L.rows < L.P ? pb + u * L.rows : L.P - 1;
+      rv[u] = ld4(L.a + p * L.a_ps + c);
+    }
+  } else if (L.rx) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      const int64_t p = pb + u * L.rows < L.P ? pb + u * L.rows : L.P - 1;
+      rv[u] = ld4(L.rx + p * L.rx_ps + c);
     }
   }
 #pragma unroll
@@ -667,16 +682,27 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
     for (int64_t pb = p0 + r; pb < p1; pb += (int64_t)kApplyU * L.rows) {
       f4 xv[kApplyU], gv[kApplyU], yv[kApplyU], rv[kApplyU];
       uint32_t mv[kApplyU];
+      // unconditional loads (pixels past p1 re-read p1 - 1, not summed), uniform branches
+      // outside the pixel loop: all pixels' loads in flight together
+      int64_t pp[kApplyU];
+#pragma unroll
+      for (int u = 0; u < kApplyU; ++u) pp[u] = pb + u * L.rows < p1 ? pb + u * L.rows : p1 - 1;
 #pragma unroll
       for (int u = 0; u < kApplyU; ++u) {
-        const int64_t p = pb + u * L.rows;
-        if (p < p1) {
-          xv[u] = ld4(L.x + p * L.x_ps + c);
-          gv[u] = ld4(L.dy + p * L.dy_ps + c);
-          if (y) yv[u] = ld4(y + p * L.a_ps + c);
-          if (mk) mv[u] = mk[p * c4 + (c >> 2)];
-          if (rb) rv[u] = ld4(L.rx + p * L.rx_ps + c);
-        }
+        xv[u] = ld4(L.x + pp[u] * L.x_ps + c);
+        gv[u] = ld4(L.dy + pp[u] * L.dy_ps + c);
+      }
+      if (y) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) yv[u] = ld4(y + pp[u] * L.a_ps + c);
+      }
+      if (mk) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) mv[u] = mk[pp[u] * c4 + (c >> 2)];
+      }
+      if (rb) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) rv[u] = ld4(L.rx + pp[u] * L.rx_ps + c);
       }
 #pragma unroll
       for (int u = 0; u < kApplyU; ++u) {
@@ -738,11 +764,41 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   const int tid = threadIdx.x;
   if (tid >= L.rows * c4) return;
   const int r = tid / c4, c = 4 * (tid - r * c4);
-  const double count = L.countp ? *L.countp : L.count;
-  const float inv_n = (float)(1.0 / count);
   const uint8_t* mk = L.relu ? L.mk : nullptr;  // stored mask, else y, else from x
   const float* y = L.relu && !mk ? L.a : nullptr;
   const bool rb = L.rx != nullptr;
+  // the pixels' loads first (unconditional: pixels past P re-read P-1, never stored; the
+  // uniform branches outside the pixel loop), then the per-channel coefficients
+  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
+  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU], rxv[kApplyU];
+  uint32_t mv[kApplyU];
+  int64_t pp[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) pp[u] = pb + u * L.rows < L.P ? pb + u * L.rows : L.P - 1;
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    gv[u] = ld4(L.dy + pp[u] * L.dy_ps + c);
+    xv[u] = ld4(L.x + pp[u] * L.x_ps + c);
+  }
+  if (y) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) yv[u] = ld4(y + pp[u] * L.a_ps + c);
+  }
+  if (mk) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) mv[u] = mk[pp[u] * c4 + (c >> 2)];
+  }
+  if (rb) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) rxv[u] = ld4(L.rx + pp[u] * L.rx_ps + c);
+  }
+  f4 dv[kApplyU];  // the residual gradient accumulated onto (dres_acc)
+  if (L.dres && L.dres_acc) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) dv[u] = ld4(L.dres + pp[u] * L.dres_ps + c);
+  }
+  const double count = L.countp ? *L.countp : L.count;
+  const float inv_n = (float)(1.0 / count);
   f4 mean, invstd, sc, sh, mg, mgx, k4;
   f4 rmean = {0.f, 0.f, 0.f, 0.f}, rinv = rmean, rmg = rmean, rmgx = rmean, rk4 = rmean;
 #pragma unroll
@@ -763,20 +819,6 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
       rk4[k] = (L.rgamma ? L.rgamma[ch] : 1.f) * rinv[k];
     }
   }
-  const int64_t pb = (int64_t)blk * L.rows * kApplyU + r;
-  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU], rxv[kApplyU];
-  uint32_t mv[kApplyU];
-#pragma unroll
-  for (int u = 0; u < kApplyU; ++u) {
-    const int64_t p = pb + u * L.rows;
-    if (p < L.P) {
-      gv[u] = ld4(L.dy + p * L.dy_ps + c);
-      xv[u] = ld4(L.x + p * L.x_ps + c);
-      if (y) yv[u] = ld4(y + p * L.a_ps + c);
-      if (mk) mv[u] = mk[p * c4 + (c >> 2)];
-      if (rb) rxv[u] = ld4(L.rx + p * L.rx_ps + c);
-    }
-  }
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u) {
     const int64_t p = pb + u * L.rows;
@@ -792,7 +834,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
     }
     if (L.dres) {
       float* dr = L.dres + p * L.dres_ps + c;
-      st4(dr, L.dres_acc ? g + ld4(dr) : g, c, C);
+      st4(dr, L.dres_acc ? g + dv[u] : g, c, C);
     }
     st4(L.o + p * L.o_ps + c, o, c, C);
     if (rb) {  // the residual BN's input gradient from the same g (bn_bwd_apply's formula)
