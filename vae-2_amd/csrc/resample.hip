@@ -335,27 +335,47 @@ __global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* 
     uint32_t ox = p - row * (uint32_t)yd.w;
     uint32_t n = hdiv.div(row);
     uint32_t oy = row - n * (uint32_t)yd.h;
-    float acc = 0.f;
+    // every term's loads first (a term's loads consumed inside its own branch were waited
+    // for before the next term's went out: one round trip per term), then the arithmetic
+    // in the same order as before (bit for bit)
+    float xv[4][4], wt[4][4], scl[4], shf[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (k >= t.n) break;
       const Act& d = t.d[k];
       const float* sv = t.sv[k];
-      float v;
       if (d.h == yd.h && d.w == yd.w) {
-        v = term_at(t.x[k], sv, (int64_t)p * d.ps + c, (int)c, (int)C);
-      } else if (!sv) {
-        v = bilinear_at(t.x[k], d, n, oy, ox, c, (float)d.h / (float)yd.h,
-                        (float)d.w / (float)yd.w);
-      } else {  // bilinear_at of the normalised taps
+        xv[k][0] = t.x[k][(int64_t)p * d.ps + c];
+      } else {
         const Lerp ly = lerp_index(oy, (int)d.h, (float)d.h / (float)yd.h);
         const Lerp lx = lerp_index(ox, (int)d.w, (float)d.w / (float)yd.w);
-        const float* base = t.x[k] + (int64_t)n * d.h * d.w * d.ps;
-        const float x00 = term_at(base, sv, ((int64_t)ly.i0 * d.w + lx.i0) * d.ps + c, (int)c, (int)C);
-        const float x01 = term_at(base, sv, ((int64_t)ly.i0 * d.w + lx.i1) * d.ps + c, (int)c, (int)C);
-        const float x10 = term_at(base, sv, ((int64_t)ly.i1 * d.w + lx.i0) * d.ps + c, (int)c, (int)C);
-        const float x11 = term_at(base, sv, ((int64_t)ly.i1 * d.w + lx.i1) * d.ps + c, (int)c, (int)C);
-        v = ly.l0 * (lx.l0 * x00 + lx.l1 * x01) + ly.l1 * (lx.l0 * x10 + lx.l1 * x11);
+        const float* base = t.x[k] + (int64_t)n * d.h * d.w * d.ps + c;
+        xv[k][0] = base[((int64_t)ly.i0 * d.w + lx.i0) * d.ps];
+        xv[k][1] = base[((int64_t)ly.i0 * d.w + lx.i1) * d.ps];
+        xv[k][2] = base[((int64_t)ly.i1 * d.w + lx.i0) * d.ps];
+        xv[k][3] = base[((int64_t)ly.i1 * d.w + lx.i1) * d.ps];
+        wt[k][0] = ly.l0; wt[k][1] = ly.l1; wt[k][2] = lx.l0; wt[k][3] = lx.l1;
+      }
+      if (sv) {
+        scl[k] = sv[2 * C + c];
+        shf[k] = sv[3 * C + c];
+      }
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= t.n) break;
+      const Act& d = t.d[k];
+      const bool bn = t.sv[k] != nullptr;
+      float v;
+      if (d.h == yd.h && d.w == yd.w) {
+        v = bn ? __builtin_fmaf(xv[k][0], scl[k], shf[k]) : xv[k][0];
+      } else {
+        float q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = bn ? __builtin_fmaf(xv[k][e], scl[k], shf[k]) : xv[k][e];
+        v = wt[k][0] * (wt[k][2] * q[0] + wt[k][3] * q[1]) +
+            wt[k][1] * (wt[k][2] * q[2] + wt[k][3] * q[3]);
       }
       acc = (k == 0) ? v : acc + v;
     }
