@@ -78,7 +78,8 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * waves of one row each (512 threads) instead of 4 waves of two rows; key 3 = 1: the
  * 18 / 36 / 72-channel 3x3 weight gradients spread their column tiles over 8 waves;
  * key 4 = the persistent 1x1 GEMM's maximum N tiles (of 16 channels) per workgroup, 3..8
- * (default 4).  Returns the previous value, -1 for an unknown key.                      */
+ * (default 4); key 5 = 1: its row tiles of 16 instead of 32 pixels; key 6 = 1: gather-GEMM
+ * convs with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder columns).  Returns the previous value, -1 for an unknown key.                      */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
@@ -440,7 +441,10 @@ int vae2_fuse_sum_relu_bn(int n, const float* const* xs, const vae2_act* xds,
  * halving source resolutions); bit 2 = the two-pass (horizontal, then vertical through a
  * workspace) power-of-two adjoint instead of the one-pass band kernel; bit 3 = the
  * LDS-staged up-sum instead of the one-pass kernel; bits 4 / 5 = 4 instead of 2 pixels in
- * flight per thread in the head backward reduce / apply passes; bits 8-15 = the
+ * flight per thread in the head backward reduce / apply passes; bit 6 = the fuse layers'
+ * pow2 adjoints through the one-pass band kernel (off by default); bit 7 = the scalar
+ * ReLU-backward (dual)
+ * kernel instead of the channel-quad one; bits 8-15 = the
  * one-pass kernel's dy rows per workgroup (a multiple of 8; 0 = 32).  Returns the
  * previous setting.  Process-wide.                                                    */
 int vae2_heads_set_algo(int algo);

@@ -518,6 +518,25 @@ def test_igemm_ksplit_conv_bn_and_accumulating_dgrad(shape, ksplit):
         lib.vae2_conv2d_set_algo(prev)
 
 
+@pytest.mark.parametrize("shape", [
+    # N, H, W, Cin, Cout, k, stride: forward N = Cout, data gradient N = Cin
+    (2, 32, 64, 36, 18, 3, 1), (2, 32, 64, 18, 36, 3, 2), (2, 24, 40, 36, 36, 1, 1),
+    (3, 17, 23, 18, 18, 3, 2)])
+def test_igemm_valu_remainder(shape):
+    """The gather kernel with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder
+    columns, vae2_conv2d_set_tune key 6; gather kernel only, K split off so it applies):
+    conv_bn training output, running statistics (the remainder columns' partial rows),
+    input / weight / BN gradients against PyTorch, and the data gradient accumulated onto
+    a prefilled buffer (beta = 1), incl. the stride-2 parity classes."""
+    from vae2 import _lib
+    lib = _lib.load()
+    prev_nr = lib.vae2_conv2d_set_tune(6, 1)
+    try:
+        test_igemm_ksplit_conv_bn_and_accumulating_dgrad(shape, False)
+    finally:
+        lib.vae2_conv2d_set_tune(6, prev_nr)
+
+
 def test_conv_bn_eval():
     from vae2 import ops
     torch.manual_seed(2)
@@ -624,6 +643,56 @@ def test_upsample_bwd_pow2_betas_and_order():
         assert rel(nchw(d), r) < 1e-6
     bad = (Act * 1)(Act(n, 3, 5, c, c))
     assert lib.vae2_upsample_bilinear_bwd_pow2_ws_size(ctypes.byref(ga), 1, bad) == -1
+
+
+@pytest.mark.parametrize("c,H,W", [(18, 16, 64), (36, 40, 128), (72, 8, 64)])
+def test_upsample_bwd_pow2_one_pass_route(c, H, W):
+    """The fuse layers' pow2 adjoint routed through the heads' one-pass band kernel
+    (targets 2 / 4 / 8 in order, 64-pixel rows; betas accumulate) against torch's adjoint,
+    and against the two-pass form (vae2_heads_set_algo bit 2)."""
+    import ctypes
+    from vae2 import ops
+    from vae2._lib import Act, call, load
+    lib = load()
+    torch.manual_seed(c + H)
+    n = 2
+    dy = torch.randn(n, c, H, W)
+    betas = [0.0, 1.0, 0.5]
+    ref, prev = [], []
+    for s, b in enumerate(betas):
+        z = torch.zeros(n, c, H >> (s + 1), W >> (s + 1), requires_grad=True)
+        F.interpolate(z, size=[H, W], mode="bilinear").backward(dy)
+        p0 = torch.randn(z.shape)
+        prev.append(p0)
+        ref.append(z.grad + b * p0)
+    g = ops.new_act((n, H, W, c), torch.empty(0, device=DEV))
+    g.copy_(nhwc(dy))
+    gp, ga = ops.act_of(g)
+    outs = []
+    try:
+        for algo in (64, 4):  # bit 6: the one-pass route (off by default); bit 2: two-pass
+            lib.vae2_heads_set_algo(algo)
+            dxs = []
+            for p0 in prev:
+                d = ops.new_act(tuple(nhwc(p0).shape), g)
+                d.copy_(nhwc(p0))
+                dxs.append(d)
+            views = [ops.act_of(d) for d in dxs]
+            acts = (Act * 3)(*[a for _, a in views])
+            wsz = lib.vae2_upsample_bilinear_bwd_pow2_ws_size(ctypes.byref(ga), 3, acts)
+            ws = torch.empty(wsz, device=DEV)
+            bt = (ctypes.c_float * 3)(*betas)
+            ptrs = (ctypes.c_void_p * 3)(*[p for p, _ in views])
+            call("vae2_upsample_bilinear_bwd_pow2", gp, ctypes.byref(ga), 3, ptrs, acts, bt,
+                 ws.data_ptr(), wsz, None)
+            torch.cuda.synchronize()
+            for d, r in zip(dxs, ref):
+                assert rel(nchw(d), r) < 1e-6, (algo, rel(nchw(d), r))
+            outs.append([d.cpu() for d in dxs])
+    finally:
+        lib.vae2_heads_set_algo(0)
+    for a, b in zip(*outs):
+        assert rel(a, b) < 1e-6
 
 
 def test_cat_codemap_and_avgpool():
@@ -845,10 +914,23 @@ GEMM1_SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("tune", [(), ((4, 8), (5, 1))], ids=["default", "tn8-tm1"])
 @pytest.mark.parametrize("shape", GEMM1_SHAPES)
-def test_gemm1x1(shape):
+def test_gemm1x1(shape, tune):
     """Forward (+ BN statistics through conv_bn), data gradient (+ beta = 1 accumulation
-    of a GradLink) and weight gradient against PyTorch fp32 on the CPU."""
+    of a GradLink) and weight gradient against PyTorch fp32 on the CPU; also with the
+    8-N-tile, 16-row-tile instances (vae2_conv2d_set_tune keys 4 / 5)."""
+    from vae2 import _lib
+    lib = _lib.load()
+    prev = [(k, lib.vae2_conv2d_set_tune(k, v)) for k, v in tune]
+    try:
+        _gemm1x1_case(shape)
+    finally:
+        for k, v in reversed(prev):
+            lib.vae2_conv2d_set_tune(k, v)
+
+
+def _gemm1x1_case(shape):
     from vae2 import ops, prof
     torch.manual_seed(8)
     n, h, w, cin, cout, bias = shape

@@ -153,6 +153,12 @@ __device__ constexpr float hat_w(int d, int f) {
   return 1.f - (float)(2 * d + 1 - f < 0 ? f - 1 - 2 * d : 2 * d + 1 - f) / (float)(2 * f);
 }
 
+// Internal (heads.hip): the fuse layers' pow2 upsampling adjoint through the one-pass
+// kernel, or -1 when its shape rules do not hold.
+int adj3_fuse_launch(const float* dy, const vae2_act* dyd, int n, float* const* dxs,
+                     const vae2_act* dxds, const float* betas, hipStream_t st);
+extern int g_relu_dual_q;  // heads.hip: vae2_heads_set_algo bit 7 clears it
+
 // Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream);

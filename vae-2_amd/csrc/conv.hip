@@ -160,7 +160,12 @@ struct IGemm {
 // KS = 4: in-workgroup K split for layers with too few row tiles to fill the chip: the 4
 // waves share one (16*TM)-row tile, wave w takes K chunks w, w+4, ..., and the partial
 // tiles are summed in LDS in a fixed order (deterministic) before wave 0's epilogue.
-template <int TM, int TN, bool VEC, int ROLE, int KS = 1, bool BF = false>
+// NR > 0 (fp32, KS = 1, one N block): N = 16*TN + NR (18 = 16 + 2, 36 = 32 + 4) -- the
+// last NR output channels on the VALU beside the MFMAs instead of a mostly-padding MFMA
+// column tile: every lane already holds its A fragment (pixel r, 4 channels of the chunk),
+// multiplies it with the remainder rows' weights for those channels, and the 4 lane
+// groups' K shares are summed at the end (dconv3_kernel's remainder, for the gather GEMM).
+template <int TM, int TN, bool VEC, int ROLE, int KS = 1, bool BF = false, int NR = 0>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   IGemm p = pin;
   if (gridDim.z > 1) {
@@ -170,7 +175,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
     p.y_offh = c.y_offh; p.y_offw = c.y_offw; p.hw_div = c.hw_div; p.w_div = c.w_div;
   }
   constexpr int BN = 16 * TN;
-  __shared__ float red[4][2][BN];
+  static_assert(NR == 0 || (KS == 1 && !BF && NR <= 4), "remainder form");
+  __shared__ float red[4][2][BN + NR];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int M = p.g_n * p.g_h * p.g_w;
@@ -202,6 +208,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   uint32_t wrow[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) wrow[j] = (uint32_t)((n0 + j * 16 + r) * kk4) * 4u;
+  uint32_t wrowr[NR > 0 ? NR : 1];  // remainder rows BN + q of the packed weights
+#pragma unroll
+  for (int q = 0; q < NR; ++q) wrowr[q] = (uint32_t)((n0 + BN + q) * kk4) * 4u;
+  float racc[TM][NR > 0 ? NR : 1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < NR; ++q) racc[i][q] = 0.f;
 
   const int ntaps = p.nth * p.ntw;
   const int K = ntaps * p.a_c4;
@@ -211,13 +225,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   const bool cpad = (p.a_c & 3) != 0;
 
   f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  f4 fr0[NR > 0 ? NR : 1], fr1[NR > 0 ? NR : 1];  // remainder weights of the chunk
   f4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  auto load = [&](f4* fa, f4* fb, int& mk) {
+  auto load = [&](f4* fa, f4* fb, f4* fr, int& mk) {
     const bool tv = tt < ntaps;
     const int tc = tv ? tt : 0;
     const int th = tc / p.ntw;
@@ -227,6 +242,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
     const uint32_t woff = tv ? (uint32_t)(tlin * p.a_c4 + c0) * 4u : kOOB;
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
+#pragma unroll
+    for (int q = 0; q < NR; ++q) fr[q] = load4(wrsrc, tv ? wrowr[q] + woff : kOOB);
     const int doff = dh * p.a_w + dw;
     const bool m1 = c0 + 1 < p.a_c, m2 = c0 + 2 < p.a_c, m3 = c0 + 3 < p.a_c;
 #pragma unroll
@@ -252,7 +269,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   };
   // Masking the pad lanes here (not right after the loads) keeps the next chunk's
   // loads in flight across this chunk's MFMAs.
-  auto mma = [&](f4* fa, const f4* fb, int mk) {
+  auto mma = [&](f4* fa, const f4* fb, const f4* fr, int mk) {
     if (VEC && cpad) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -268,22 +285,28 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) racc[i][q] = __builtin_fmaf(fa[i][s], fr[q][s], racc[i][q]);
   };
 
   // Chunk pairs; the (possibly) extra odd chunk loads zeros (tt >= ntaps).
   if (mw < M && !BF) {
     int mk0 = 0, mk1 = 0;
-    load(fa0, fb0, mk0);
+    load(fa0, fb0, fr0, mk0);
     for (int ch = 0; ch < nchunks; ch += 2) {
-      load(fa1, fb1, mk1);
-      mma(fa0, fb0, mk0);
-      load(fa0, fb0, mk0);
-      mma(fa1, fb1, mk1);
+      load(fa1, fb1, fr1, mk1);
+      mma(fa0, fb0, fr0, mk0);
+      load(fa0, fb0, fr0, mk0);
+      mma(fa1, fb1, fr1, mk1);
     }
   } else if (mw < M) {  // bf16 operands: one 16x16x32 MFMA per chunk pair
     int mk0 = 0, mk1 = 0;
-    load(fa0, fb0, mk0);
-    load(fa1, fb1, mk1);
+    load(fa0, fb0, fr0, mk0);
+    load(fa1, fb1, fr1, mk1);
     for (int ch = 0; ch < nchunks; ch += 2) {
       if (VEC && cpad) {
 #pragma unroll
@@ -301,8 +324,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       for (int i = 0; i < TM; ++i) A[i] = pack_bf16(fa0[i], fa1[i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) B[j] = pack_bf16(fb0[j], fb1[j]);
-      load(fa0, fb0, mk0);
-      load(fa1, fb1, mk1);
+      load(fa0, fb0, fr0, mk0);
+      load(fa1, fb1, fr1, mk1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -425,6 +448,43 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       }
     }
   }
+  // the VALU remainder's outputs: the 4 lane groups' K shares summed (every group then holds
+  // pixel i*16 + r's sums); lane group g writes the channels q = g (mod 4)
+  float rsum[NR > 0 ? NR : 1], rsq[NR > 0 ? NR : 1];
+  if constexpr (NR > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        racc[i][q] += __shfl_xor(racc[i][q], 16, 64);
+        racc[i][q] += __shfl_xor(racc[i][q], 32, 64);
+      }
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      rsum[q] = 0.f;
+      rsq[q] = 0.f;
+      if ((q & 3) != g) continue;
+      const int n = n0 + BN + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mw + i * 16 + r;
+        const bool mok = m < M && n < p.n;
+        const int mm = m < M ? m : 0;
+        const int gn = (int)p.hw_div.div((uint32_t)mm);
+        const int rem = mm - gn * p.g_h * p.g_w;
+        const int gi = (int)p.w_div.div((uint32_t)rem);
+        const int gj = rem - gi * p.g_w;
+        float* yp = p.y + ((gn * p.y_h + gi * p.y_step + p.y_offh) * p.y_w + gj * p.y_step +
+                           p.y_offw) * p.y_ps + n;
+        float v = racc[i][q];
+        if (p.bias) v += p.bias[n < p.n ? n : 0];
+        if (p.beta != 0.f && mok) v += p.beta * *yp;
+        if (mok) *yp = v;
+        rsum[q] += mok ? v : 0.f;
+        rsq[q] += mok ? v * v : 0.f;
+      }
+    }
+  }
   if (p.stats) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -432,6 +492,24 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       csum[j] += __shfl_xor(csum[j], 32, 64);
       csq[j] += __shfl_xor(csq[j], 16, 64);
       csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if constexpr (NR > 0) {  // sum over the wave's pixels (the 16 lanes r of group g)
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          rsum[q] += __shfl_xor(rsum[q], o, 64);
+          rsq[q] += __shfl_xor(rsq[q], o, 64);
+        }
+      }
+      if (r == 0) {
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+          if ((q & 3) != g) continue;
+          red[wave][0][BN + q] = rsum[q];
+          red[wave][1][BN + q] = rsq[q];
+        }
+      }
     }
     if (KS > 1) {  // wave 0 holds the whole row tile
       if (g == 0) {
@@ -455,7 +533,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
     }
     __syncthreads();
     const int rows = gridDim.x;
-    for (int c = threadIdx.x; c < BN; c += 256) {
+    for (int c = threadIdx.x; c < BN + NR; c += 256) {
       if (n0 + c >= p.n) continue;
       float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
       float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
@@ -1230,6 +1308,7 @@ __global__ __launch_bounds__(256) void dconv3_group_kernel(DConvGroup gp) {
 struct Tile {
   int tm, tn, nblk;
   int ks = 1;  // in-workgroup K split (igemm_kernel KS)
+  int nr = 0;  // output channels on the VALU beside the MFMA columns (igemm_kernel NR)
 };
 
 // Rows per workgroup and the K split: layers whose row tiles would leave the chip with
@@ -1259,9 +1338,12 @@ int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients ov
 // LDS-sized grid) -> 157 (TN 8) -> 131 us (TN 4, 152 VGPRs), 256->64 data gradient
 // 153 -> 127 us; step 845.1 / 845.4 (8) vs 847.3 / 848.0 frames/s (4), same box.
 int g_gemm1_tn = 4;
+int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 16 * TM pixels (1, 2)
+int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
-    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn;
+    g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
+    g_gemm1_tm, g_igemm_nr;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1303,6 +1385,12 @@ static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   const int64_t blocks = ceil_div(M, 64 * t.tm) * t.nblk * ncls;
   const int chunks = (taps * k4 + 15) / 16;
   if (g_ksplit && !wide && blocks < 512 && chunks >= 16) t.ks = 4;
+  // tune key 6: 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder, fp32, no K split)
+  if (g_igemm_nr && !g_bf16 && t.ks == 1 && !wide && (N == 18 || N == 36)) {
+    t.tn = N == 18 ? 1 : 2;
+    t.nr = N == 18 ? 2 : 4;
+    t.nblk = 1;
+  }
   return t;
 }
 
@@ -1313,10 +1401,10 @@ static bool vec_ok(const float* a, int ps) {
 
 // ---------------------------------------------------- 1x1 GEMM: host dispatch ----
 struct G1Tile {
-  int tn, nblk, grid_x;
+  int tm = 2, tn, nblk, grid_x;
   size_t lds;
 };
-int gemm1_blocks_per_cu(int tn, size_t lds);
+int gemm1_blocks_per_cu(int tm, int tn, size_t lds);
 
 static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
                        const float* a, G1Tile* out) {
@@ -1337,8 +1425,9 @@ static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride
   if (t.lds > 96 * 1024) return false;
   // resident workgroups per CU (registers and LDS; the TN = 8 instance holds 264 VGPRs:
   // one wave per SIMD) -- the persistent grid is exactly that many per CU
-  const int per_cu = gemm1_blocks_per_cu(t.tn, t.lds);
-  const int64_t ntiles = ceil_div(M, 32);
+  t.tm = g_gemm1_tm == 1 ? 1 : 2;  // tune key 5: 16-row tiles (half the accumulators)
+  const int per_cu = gemm1_blocks_per_cu(t.tm, t.tn, t.lds);
+  const int64_t ntiles = ceil_div(M, 16 * t.tm);
   int64_t gx = 256 * per_cu / t.nblk;
   if (gx > ceil_div(ntiles, 4)) gx = ceil_div(ntiles, 4);
   t.grid_x = (int)(gx < 1 ? 1 : gx);
@@ -1380,7 +1469,21 @@ static void launch_wide(const IGemm& p, int tn, dim3 grid, hipStream_t s) {
 }
 
 template <bool VEC, int ROLE>
+static void launch_nr(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
+#define NRL(TM_)                                                                             \
+  if (t.nr == 2) VAE2_LAUNCH((igemm_kernel<TM_, 1, VEC, ROLE, 1, false, 2>), grid, dim3(256), 0, s, p); \
+  else VAE2_LAUNCH((igemm_kernel<TM_, 2, VEC, ROLE, 1, false, 4>), grid, dim3(256), 0, s, p);
+  if (t.tm == 4) { NRL(4) }
+  else if (t.tm == 2) { NRL(2) }
+  else { NRL(1) }
+#undef NRL
+}
+template <bool VEC, int ROLE>
 static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
+  if (t.nr) {
+    launch_nr<VEC, ROLE>(p, t, grid, s);
+    return;
+  }
   if (t.ks > 1) {  // (never with wide tiles: those need >= 65536 rows)
     if (t.tm == 4) launch_tn<4, VEC, ROLE, 4>(p, t.tn, grid, s);
     else if (t.tm == 2) launch_tn<2, VEC, ROLE, 4>(p, t.tn, grid, s);
@@ -2119,33 +2222,35 @@ static uint32_t act_bytes(const vae2_act* d) {
 }
 
 #if VAE2_PART(1)
-// hipOccupancyMaxActiveBlocksPerMultiprocessor of gemm1x1_kernel<2, tn> with `lds` bytes
-// of dynamic LDS (cached per (tn, lds)); at least 1.
-int gemm1_blocks_per_cu(int tn, size_t lds) {
-  static int cache[9][4] = {};
-  static size_t cache_lds[9][4] = {};
-  if (tn < 3 || tn > 8) return 1;
+// hipOccupancyMaxActiveBlocksPerMultiprocessor of gemm1x1_kernel<tm, tn> with `lds` bytes
+// of dynamic LDS (cached per (tm, tn, lds)); at least 1.
+int gemm1_blocks_per_cu(int tm, int tn, size_t lds) {
+  static int cache[3][9][4] = {};
+  static size_t cache_lds[3][9][4] = {};
+  if (tn < 3 || tn > 8 || tm < 1 || tm > 2) return 1;
   for (int i = 0; i < 4; ++i)
-    if (cache[tn][i] && cache_lds[tn][i] == lds) return cache[tn][i];
+    if (cache[tm][tn][i] && cache_lds[tm][tn][i] == lds) return cache[tm][tn][i];
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
-  switch (tn) {
-#define CASE(T)                                                                          \
+#define CASE(M, T)                                                                       \
   case T:                                                                                \
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(                                    \
-        &n, reinterpret_cast<const void*>(gemm1x1_kernel<2, T>), 256, lds);              \
+        &n, reinterpret_cast<const void*>(gemm1x1_kernel<M, T>), 256, lds);              \
     break;
-    CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-#undef CASE
+  if (tm == 1) {
+    switch (tn) { CASE(1, 3) CASE(1, 4) CASE(1, 5) CASE(1, 6) CASE(1, 7) CASE(1, 8) }
+  } else {
+    switch (tn) { CASE(2, 3) CASE(2, 4) CASE(2, 5) CASE(2, 6) CASE(2, 7) CASE(2, 8) }
   }
+#undef CASE
   if (e != hipSuccess || n < 1) {
     (void)hipGetLastError();
     n = 1;
   }
   for (int i = 0; i < 4; ++i)
-    if (!cache[tn][i]) {
-      cache[tn][i] = n;
-      cache_lds[tn][i] = lds;
+    if (!cache[tm][tn][i]) {
+      cache[tm][tn][i] = n;
+      cache_lds[tm][tn][i] = lds;
       break;
     }
   return n;
@@ -2165,13 +2270,20 @@ int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.w = wp; p.n = (int)yd->c; p.bias = bias; p.y = y; p.y_ps = (int)yd->ps; p.beta = beta;
   p.stats = stats; p.a_bytes = act_bytes(ad); p.w_bytes = w_bytes;
   const dim3 grid((unsigned)t.grid_x, (unsigned)t.nblk);
-  switch (t.tn) {
-#define CASE(T) \
-  case T: VAE2_LAUNCH((gemm1x1_kernel<2, T>), grid, dim3(256), t.lds, s, p); break;
-    CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-#undef CASE
-    default: return fail(fn, "gemm1x1: unsupported N block");
+#define CASE(M, T) \
+  case T: VAE2_LAUNCH((gemm1x1_kernel<M, T>), grid, dim3(256), t.lds, s, p); break;
+  if (t.tm == 1) {
+    switch (t.tn) {
+      CASE(1, 3) CASE(1, 4) CASE(1, 5) CASE(1, 6) CASE(1, 7) CASE(1, 8)
+      default: return fail(fn, "gemm1x1: unsupported N block");
+    }
+  } else {
+    switch (t.tn) {
+      CASE(2, 3) CASE(2, 4) CASE(2, 5) CASE(2, 6) CASE(2, 7) CASE(2, 8)
+      default: return fail(fn, "gemm1x1: unsupported N block");
+    }
   }
+#undef CASE
   return check_launch(fn);
 }
 
@@ -2633,6 +2745,16 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_gemm1_tn = value >= 3 && value <= 8 ? value : 4;
     return prev;
   }
+  if (key == 5) {
+    const int prev = g_gemm1_tm;
+    g_gemm1_tm = value == 1 ? 1 : 2;
+    return prev;
+  }
+  if (key == 6) {
+    const int prev = g_igemm_nr;
+    g_igemm_nr = value ? 1 : 0;
+    return prev;
+  }
   return -1;
 }
 
@@ -2745,7 +2867,7 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
   }
   G1Tile g1;
   if (gemm1_pick(xd, yd, k, stride, pad, (const float*)16, &g1)) {
-    snprintf(buf, (size_t)len, "gemm1x1_kernel<2, %d>", g1.tn);
+    snprintf(buf, (size_t)len, "gemm1x1_kernel<%d, %d>", g1.tm, g1.tn);
     return 0;
   }
   Tile t = pick_igemm_tile(act_pixels(yd), (int)yd->c, k * k, round_up((int)xd->c, 4), 1);

@@ -739,6 +739,7 @@ struct UpAdj {
   int zh[3], zw[3], dx_ps[3];
   float sh[3], sw[3];
   int halo, nxb;
+  float beta[3];  // up_adj3_kernel: dx_s = adjoint + beta_s * dx_s (the fuse adjoints)
 };
 
 __device__ __forceinline__ void adj_window(int i, int in_size, int out_size, float scale,
@@ -1005,6 +1006,11 @@ __global__ __launch_bounds__(256) void up_adj2_v_kernel(UpAdj p) {
 static int g_adj_stream = 1;  // vae2_heads_set_algo bit 0 clears it
 static int g_upsum_tight = 1;  // vae2_heads_set_algo bit 1 clears it
 static int g_upsum_one = 1;    // vae2_heads_set_algo bit 3 clears it (upsum2_kernel)
+// vae2_heads_set_algo bit 6 sets it: the fuse adjoints (resample.hip) through the one-pass
+// band kernel -- off: with 18-72 channels a 64-lane channel block is mostly idle and the
+// step measured 851-853 vs 861-866 frames/s through the two-pass quad kernels (A/B, same box)
+int g_fuse_adj3 = 0;
+int g_relu_dual_q = 1;         // vae2_heads_set_algo bit 7 clears it (relu_bwd_dual quad form)
 static int g_head_red_u = 2;   // vae2_heads_set_algo bit 4: 4 pixels in flight (backward reduce)
 static int g_head_app_u = 2;   // vae2_heads_set_algo bit 5: 4 pixels in flight (backward apply)
 
@@ -1089,6 +1095,16 @@ __device__ __forceinline__ void adj3_store(const Adj3Src<S>& a, const UpAdj& p, 
   if (!cok || iy < b0 / F || iy >= b1 / F) return;
   float* out = p.dx[S] + ((int64_t)n * p.zh[S] + iy) * p.zw[S] * p.dx_ps[S] + c;
   const int ix0 = px0 / F;
+  const float beta = p.beta[S];
+  if (beta != 0.f) {
+    float old[Adj3Src<S>::J];
+#pragma unroll
+    for (int j = 0; j < Adj3Src<S>::J; ++j) old[j] = out[(int64_t)(ix0 + j) * p.dx_ps[S]];
+#pragma unroll
+    for (int j = 0; j < Adj3Src<S>::J; ++j)
+      out[(int64_t)(ix0 + j) * p.dx_ps[S]] = a.lo[j] + beta * old[j];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < Adj3Src<S>::J; ++j) out[(int64_t)(ix0 + j) * p.dx_ps[S]] = a.lo[j];
 }
@@ -1204,6 +1220,33 @@ static bool adj_one_pass(const vae2_act* dyd, int n, const vae2_act* dxds) {
     if (!act_ok(&dxds[s]) || dyd->w != dxds[s].w << (s + 1) || dyd->h != dxds[s].h << (s + 1))
       return false;
   return true;
+}
+
+// The fuse layers' power-of-two adjoints (resample.hip, vae2_upsample_bilinear_bwd_pow2)
+// through the one-pass kernel when its shape rules hold (targets of exactly 2 / 4 / 8, in
+// that order; 64-pixel chunks); -1 when they do not (the caller takes its two-pass path).
+int adj3_fuse_launch(const float* dy, const vae2_act* dyd, int n, float* const* dxs,
+                     const vae2_act* dxds, const float* betas, hipStream_t st) {
+  if (!g_adj_fused || !g_fuse_adj3 || n < 1 || n > 3 || !adj_one_pass(dyd, n, dxds)) return -1;
+  for (int s = 0; s < n; ++s)
+    if (!dxs[s] || dxds[s].n != dyd->n || dxds[s].c != dyd->c) return -1;
+  UpAdj p{};
+  p.dy = dy; p.dy_ps = (int)dyd->ps; p.H = (int)dyd->h; p.W = (int)dyd->w; p.C = (int)dyd->c;
+  for (int s = 0; s < n; ++s) {
+    p.dx[s] = dxs[s]; p.zh[s] = (int)dxds[s].h; p.zw[s] = (int)dxds[s].w;
+    p.dx_ps[s] = (int)dxds[s].ps;
+    p.beta[s] = betas ? betas[s] : 0.f;
+  }
+  p.nxb = (int)ceil_div(dyd->w, kUsXB);
+  const int br = dyd->h < g_adj_band ? (int)dyd->h : g_adj_band;
+  const int nband = (int)ceil_div(dyd->h, br);
+  const dim3 grid((unsigned)(dyd->n * nband * p.nxb * ceil_div(dyd->c, 64)));
+  switch (n) {
+    case 1: VAE2_LAUNCH(up_adj3_kernel<1>, grid, dim3(256), 0, st, p, br, nband); break;
+    case 2: VAE2_LAUNCH(up_adj3_kernel<2>, grid, dim3(256), 0, st, p, br, nband); break;
+    default: VAE2_LAUNCH(up_adj3_kernel<3>, grid, dim3(256), 0, st, p, br, nband); break;
+  }
+  return 0;
 }
 
 // Pixels per block of the backward passes (>= 64 each): the reduce pass with <= 2048
@@ -1423,13 +1466,16 @@ int64_t vae2_upsample_bilinear_bwd_multi_ws_size(const vae2_act* dyd, int n,
 int vae2_heads_set_algo(int algo) {
   const int prev = (g_adj_stream ? 0 : 1) | (g_upsum_tight ? 0 : 2) | (g_adj_fused ? 0 : 4) |
                    (g_upsum_one ? 0 : 8) | (g_head_red_u == 4 ? 16 : 0) |
-                   (g_head_app_u == 4 ? 32 : 0) | (g_adj_band == 32 ? 0 : g_adj_band << 8);
+                   (g_head_app_u == 4 ? 32 : 0) | (g_fuse_adj3 ? 64 : 0) |
+                   (g_relu_dual_q ? 0 : 128) | (g_adj_band == 32 ? 0 : g_adj_band << 8);
   g_adj_stream = (algo & 1) ? 0 : 1;
   g_upsum_tight = (algo & 2) ? 0 : 1;
   g_adj_fused = (algo & 4) ? 0 : 1;
   g_upsum_one = (algo & 8) ? 0 : 1;
   g_head_red_u = (algo & 16) ? 4 : 2;
   g_head_app_u = (algo & 32) ? 4 : 2;
+  g_fuse_adj3 = (algo & 64) ? 1 : 0;
+  g_relu_dual_q = (algo & 128) ? 0 : 1;
   const int band = (algo >> 8) & 0xff;  // one-pass adjoint band rows (0: default 32)
   g_adj_band = band >= 8 && band % 8 == 0 ? band : 32;
   return prev;

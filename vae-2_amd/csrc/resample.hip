@@ -417,6 +417,40 @@ __global__ __launch_bounds__(256) void relu_bwd_dual_kernel(
   }
 }
 
+// Channel-quad form (16-byte pixel rows): thread = (pixel, quad), one 16-byte load per
+// operand and 16-byte stores (channels past C in the last quad untouched).
+__global__ __launch_bounds__(256) void relu_bwd_dual_q_kernel(
+    const float* __restrict__ dy, Act dyd, const float* __restrict__ y, Act yd,
+    float* __restrict__ g, Act gd, float* __restrict__ g2, Act g2d, float beta2, FastDiv qdiv) {
+  const int C = (int)yd.c, Q = (C + 3) >> 2;
+  const uint32_t total = (uint32_t)(yd.n * yd.h * yd.w) * (uint32_t)Q;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t p = qdiv.div(i);
+    const int c = 4 * (int)(i - p * (uint32_t)Q);
+    const f4 dv = *reinterpret_cast<const f4*>(dy + (int64_t)p * dyd.ps + c);
+    const f4 yv = *reinterpret_cast<const f4*>(y + (int64_t)p * yd.ps + c);
+    float* d2 = g2 + (int64_t)p * g2d.ps + c;
+    f4 o2 = {0.f, 0.f, 0.f, 0.f};
+    if (beta2 != 0.f) o2 = *reinterpret_cast<const f4*>(d2);
+    f4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = yv[k] > 0.f ? dv[k] : 0.f;
+    float* d1 = g + (int64_t)p * gd.ps + c;
+    if (c + 4 <= C) {
+      *reinterpret_cast<f4*>(d1) = v;
+      *reinterpret_cast<f4*>(d2) = beta2 != 0.f ? v + beta2 * o2 : v;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < C) {
+          d1[k] = v[k];
+          d2[k] = beta2 != 0.f ? v[k] + beta2 * o2[k] : v[k];
+        }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_act_kernel(const float* __restrict__ x, Act xd,
                                                        float* __restrict__ y, Act yd, float beta,
                                                        FastDiv cdiv) {
@@ -688,6 +722,10 @@ int vae2_upsample_bilinear_bwd_pow2(const float* dy, const vae2_act* dyd, int n,
   VAE2_REQUIRE(ws_size >= need, fn, "workspace too small");
   VAE2_REQUIRE(dyd->ps % 4 == 0 && (uintptr_t)dy % 16 == 0 && (uintptr_t)ws % 16 == 0, fn,
                "dy and ws must be 16-byte aligned with a pixel stride of 4k");
+  hipStream_t st = as_stream(stream);
+  // one launch, dy read once (heads.hip's band kernel) where the targets are 2 / 4 / 8 in
+  // order and the rows are 64-pixel chunks
+  if (adj3_fuse_launch(dy, dyd, n, dxs, dxds, betas, st) == 0) return check_launch(fn);
   UpAdjQ p{};
   p.g = dy; p.g_ps = dyd->ps; p.H = (int)dyd->h; p.W = (int)dyd->w; p.C = (int)dyd->c;
   p.Q = (p.C + 3) / 4; p.nt = n; p.q_d = FastDiv((uint32_t)p.Q);
@@ -708,7 +746,6 @@ int vae2_upsample_bilinear_bwd_pow2(const float* dy, const vae2_act* dyd, int n,
     if (p.cnt_h[s] > mh) mh = p.cnt_h[s];
     if (p.cnt_v[s] > mv) mv = p.cnt_v[s];
   }
-  hipStream_t st = as_stream(stream);
   VAE2_LAUNCH(up_adjq_kernel<false>, dim3((mh + 255) / 256, n), dim3(256), 0, st, p);
   int rc = check_launch(fn);
   if (rc) return rc;
@@ -773,6 +810,16 @@ int vae2_relu_bwd_dual(const float* dy, const vae2_act* dyd, const float* y,
   VAE2_REQUIRE(same_hw(dyd, yd) && same_hw(yd, gd) && same_hw(yd, g2d) && dyd->c == yd->c &&
                    gd->c == yd->c && g2d->c == yd->c, fn, "shape mismatch");
   int64_t total = act_elems(yd);
+  auto q16 = [](const float* ptr, const vae2_act* d) {
+    return ((uintptr_t)ptr % 16 == 0) && d->ps % 4 == 0;
+  };
+  if (g_relu_dual_q && q16(dy, dyd) && q16(y, yd) && q16(g, gd) && q16(g2, g2d)) {
+    const int64_t quads = act_pixels(yd) * ((yd->c + 3) / 4);
+    VAE2_LAUNCH(relu_bwd_dual_q_kernel, dim3(ew_blocks(quads)), dim3(256), 0,
+                as_stream(stream), dy, to_act(dyd), y, to_act(yd), g, to_act(gd), g2,
+                to_act(g2d), beta2, FastDiv((uint32_t)((yd->c + 3) / 4)));
+    return check_launch(fn);
+  }
   VAE2_LAUNCH(relu_bwd_dual_kernel, dim3(ew_blocks(total)), dim3(256), 0, as_stream(stream),
               dy, to_act(dyd), y, to_act(yd), g, to_act(gd), g2, to_act(g2d), beta2,
               FastDiv((uint32_t)yd->c));
