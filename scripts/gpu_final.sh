@@ -19,3 +19,9 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --dtype bf16 \
   || { tail -20 gpurun_out/${TAG}_bench_bf16.log; exit 1; }
 grep '^{' gpurun_out/${TAG}_bench_bf16.log | cut -c1-200
 bash scripts/gpu_pmc.sh ${TAG}_bnapply bn_bwd_apply_multi_kernel
+timeout -k 10 300 python bench.py --no-cpu-baseline --dtype bf16 --height 256 --width 512 --batch 2 \
+  > gpurun_out/${TAG}_bench_bf16_256x512.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_bf16_256x512.log; exit 1; }
+grep '^{' gpurun_out/${TAG}_bench_bf16_256x512.log | cut -c1-200
+timeout -k 10 300 python bench.py --no-cpu-baseline --height 256 --width 512 --batch 2 \
+  > gpurun_out/${TAG}_bench_256x512.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_256x512.log; exit 1; }
+grep '^{' gpurun_out/${TAG}_bench_256x512.log | cut -c1-200
