@@ -6,8 +6,8 @@ TAG=${1:-lab}
 OLD=$PWD/vae-2_amd/vae2/ab/${2:-old.so}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
-  tests/test_kernels_gpu.py tests/test_lazy_bn_gpu.py -k "bn or BatchNorm or lazy or resbn or fuse" -m gpu \
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+  ${TESTS:-tests/test_kernels_gpu.py tests/test_lazy_bn_gpu.py} -k "${TESTK:-bn or BatchNorm or lazy or resbn or fuse}" -m gpu \
   > gpurun_out/${TAG}_tests.log 2>&1 || { tail -20 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
 i=0

@@ -514,9 +514,17 @@ __global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __re
     float s = 0.f;
     if (tid < S) {
       const int c = tid % C, rr = tid / C;
-      if (wr) {
-        for (int64_t p = p0 + rr; p < p1; p += R)
-          s += base[p * xd.ps + c] * (wr[p / xd.w] * wc[p % xd.w]);
+      if (wr) {  // (row, column) of p tracked incrementally: no 64-bit division per pixel
+        const int W = (int)xd.w;
+        int iy = (int)((p0 + rr) / W), ix = (int)((p0 + rr) - (int64_t)iy * W);
+        for (int64_t p = p0 + rr; p < p1; p += R) {
+          s += base[p * xd.ps + c] * (wr[iy] * wc[ix]);
+          ix += R;
+          while (ix >= W) {
+            ix -= W;
+            ++iy;
+          }
+        }
       } else {
         for (int64_t p = p0 + rr; p < p1; p += R) s += base[p * xd.ps + c];
       }
@@ -529,10 +537,17 @@ __global__ __launch_bounds__(256) void spatial_partials_kernel(const float* __re
       out[tid] = a;
     }
   } else {
+    const int W = (int)xd.w;
     for (int c = tid; c < C; c += 256) {
       float s = 0.f;
-      for (int64_t p = p0; p < p1; ++p)
-        s += base[p * xd.ps + c] * (wr ? wr[p / xd.w] * wc[p % xd.w] : 1.f);
+      int iy = (int)(p0 / W), ix = (int)(p0 - (int64_t)iy * W);
+      for (int64_t p = p0; p < p1; ++p) {
+        s += base[p * xd.ps + c] * (wr ? wr[iy] * wc[ix] : 1.f);
+        if (++ix == W) {
+          ix = 0;
+          ++iy;
+        }
+      }
       out[c] = s;
     }
   }
@@ -554,8 +569,8 @@ __global__ void spatial_finish_kernel(const float* __restrict__ part, int64_t ch
 
 static int64_t spatial_chunks(const vae2_act* xd, int64_t* ppb_out) {
   int64_t HW = xd->h * xd->w;
-  int64_t chunks = ceil_div(HW, 512);
-  if (chunks > 64) chunks = 64;
+  int64_t chunks = ceil_div(HW, 128);  // (512 / 64: 512 workgroups at 128x256 x 8 looped
+  if (chunks > 256) chunks = 256;      //  16 dependent loads per thread, 56 us per call)
   int64_t ppb = ceil_div(HW, chunks);
   if (ppb_out) *ppb_out = ppb;
   return ceil_div(HW, ppb);
