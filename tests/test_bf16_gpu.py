@@ -13,10 +13,12 @@ variant; the same step with fp32 operands keeps the fp32 bounds):
               loss within 2e-3 of the fp32 run's, every later one within 15 % (the
               trajectory is chaotic: Adam's first steps move every weight by ~lr;
               measured deviation <= 7 %).
-Per-tensor gradients are not compared: at the reference's init (conv weights std 1e-3,
-every conv followed by BatchNorm) they are chaotic — fp32 operands already land 6 %
-(median rel-L2) from the fp32 oracle by rounding order alone, and bf16 rounding
-decorrelates them (cosine 0.04 measured) while the loss trajectory is unchanged."""
+Per-tensor gradients (test_bf16_config2_per_tensor_gradients_track_fp32): on a
+Kaiming-scale state, against the fp32-operand HIP step, cosine >= 0.99 and norm within
+5 % on the tensors the reference's own fp64 step holds under a bf16-sized input
+perturbation (the output heads); the rest of this BatchNorm network's gradient is
+chaotic in its inputs in the reference's arithmetic too (tests/diag_grad_chaos.py), so
+there only the norm is bounded."""
 import pytest
 import torch
 
@@ -135,3 +137,79 @@ def test_bf16_config5_training_tracks_fp32():
     assert abs(h16[0][0] - h32[0][0]) <= 2e-3 * h32[0][0]
     for i, (a, b) in enumerate(zip(h16, h32)):
         assert abs(a[0] - b[0]) <= 0.15 * abs(b[0]), (i, a[0], b[0])
+
+
+def _kaiming_grads(bf16, xs, eps, code, seed=21):
+    """One HIP forward+backward at config 2 with every conv / linear weight re-drawn at
+    Kaiming scale (std sqrt(2 / fan_in), seeded on the CPU so both runs share it):
+    {name: fp64 gradient} from the flat main_grad buffers."""
+    from test_model_gpu import named_params
+    prev = _set_bf16(bf16)
+    try:
+        torch.manual_seed(0)
+        fm = hip_model(KW)
+        params = named_params(("encz", fm.encz_model), ("ed", fm.encdec_model))
+        gen = torch.Generator().manual_seed(seed)
+        with torch.no_grad():
+            for _, p in params:
+                if p.dim() >= 2:
+                    std = (2.0 / p[0].numel()) ** 0.5
+                    p.copy_(torch.randn(p.shape, generator=gen) * std)
+        fm.set_noise(eps, code)
+        losses = fm(*[x.to(DEV) for x in xs], 1.0)[0]
+        losses[0].backward()
+        torch.cuda.synchronize()
+        return {n: p.main_grad.detach().double().cpu().clone() for n, p in params}
+    finally:
+        _set_bf16(prev)
+
+
+# The tensors whose gradient the reference's own fp64 step holds (cosine > 0.99) when its
+# inputs carry a bf16-sized relative perturbation (2e-3) on the Kaiming-scale state of
+# _kaiming_grads: the decoders' output heads.  Measured by tests/diag_grad_chaos.py.
+STABLE = ["ed.decf_last_layer_1.1.weight", "ed.decf_last_layer_1.1.bias",
+          "ed.decf_last_layer_1.3.weight", "ed.decf_last_layer_1.3.bias",
+          "ed.decf_last_layer_2.1.bias", "ed.decf_last_layer_2.3.bias",
+          "ed.decf_last_layer_3.1.bias", "ed.decf_last_layer_3.3.bias",
+          "ed.decp_last_layer_2.1.weight", "ed.decp_last_layer_2.1.bias",
+          "ed.decp_last_layer_2.3.weight", "ed.decp_last_layer_2.3.bias",
+          "ed.decp_last_layer_3.1.weight", "ed.decp_last_layer_3.1.bias",
+          "ed.decp_last_layer_3.3.weight", "ed.decp_last_layer_3.3.bias"]
+
+
+def test_bf16_config2_per_tensor_gradients_track_fp32():
+    """Per-parameter gradients of the bf16-operand step against the fp32-operand HIP step
+    (config 2, 64x64, B=4) on Kaiming-scale weights.
+
+    Below the output heads the ELBO gradient of this BatchNorm network is chaotic in its
+    inputs, in the reference's own arithmetic: tests/diag_grad_chaos.py runs the fp64
+    oracle on this state with its inputs scaled by (1 + e * N(0,1)) and measures the
+    median per-tensor cosine to the unperturbed fp64 gradient at 0.9995 (e = 1e-7), 0.945
+    (1e-5), 0.50 (1e-4) and 0.013 (2e-3); the fp32 oracle sits at median 0.998, min
+    0.991.  A cosine bar on those tensors is unattainable for any arithmetic coarser than
+    fp32, the reference's included.  So: on the tensors the reference itself holds under
+    a bf16-sized perturbation of its inputs (STABLE) the bf16 gradient must keep median
+    cosine >= 0.99, every cosine >= 0.98 and norm within 10 % of the fp32-operand
+    gradient (measured: cosine median 0.997, min 0.989; norm ratio 0.948 .. 1.004;
+    bf16 rounds every conv operand, a larger perturbation than rounding the inputs);
+    on every other tensor (chaotic) only the gradient norm is bounded, within a factor
+    2 of the fp32-operand norm for the median tensor."""
+    xs, eps, code = _inputs(seed=17)
+    g32 = _kaiming_grads(False, xs, eps, code)
+    g16 = _kaiming_grads(True, xs, eps, code)
+    cos, nr = {}, {}
+    for n, a in g32.items():
+        b = g16[n]
+        cos[n] = float((a * b).sum() / (a.norm() * b.norm() + 1e-300))
+        nr[n] = float(b.norm() / (a.norm() + 1e-300))
+    print({n: (round(cos[n], 5), round(nr[n], 4)) for n in STABLE})
+    for n in STABLE:
+        assert cos[n] >= 0.98, (n, cos[n])
+        assert abs(nr[n] - 1) <= 0.10, (n, nr[n])
+    assert sorted(cos[n] for n in STABLE)[len(STABLE) // 2] >= 0.99
+    big = max(float(a.norm()) for a in g32.values())
+    rest = sorted(nr[n] for n, a in g32.items()
+                  if n not in STABLE and float(a.norm()) > 1e-4 * big)
+    med = rest[len(rest) // 2]
+    print(f"chaotic tensors: {len(rest)}, median norm ratio {med:.3f}")
+    assert 0.5 <= med <= 2.0, med
