@@ -68,6 +68,25 @@ def _w_invariant(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _w_ddp_guard(rank, world, port, q):
+    """The reference's train.py:225-229 call on a HIP-path model: DDP must refuse it (its
+    per-parameter hooks never fire: gradients go to main_grad); a plain module still wraps."""
+    _init(rank, world, port)
+    from helpers import build, make_cfg
+    from vae2.model import FullModel_encdec
+    from vae2.criterion import KLLoss, L1Loss
+    ed, ez = build(make_cfg("tiny"))
+    fm = FullModel_encdec(ez, ed, None, None, L1Loss(), KLLoss(), None, 1.0, 0.1, 1.0, 0.0)
+    msg = None
+    try:
+        torch.nn.parallel.DistributedDataParallel(fm, find_unused_parameters=True)
+    except RuntimeError as e:
+        msg = str(e)
+    plain = torch.nn.parallel.DistributedDataParallel(torch.nn.Linear(3, 2))
+    q.put((rank, msg, type(plain).__name__))
+    dist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -122,3 +141,11 @@ def test_decoder_tail_range_is_the_decoders():
     assert names and all(n.startswith(("decf_", "decp_")) for n in names)
     assert not any(n.startswith(("decf_", "decp_")) for n, o in zip(flat.names, flat.offsets)
                    if o < start)
+
+
+def test_ddp_refuses_hip_path_model():
+    """A reference caller that keeps DistributedDataParallel gets a clear error instead of
+    silently un-reduced gradients (vae2.dist.guard_ddp); other modules are unaffected."""
+    for _, msg, plain in _run(_w_ddp_guard):
+        assert msg is not None and "allreduce_grads" in msg and "main_grad" in msg
+        assert plain == "DistributedDataParallel"

@@ -12,8 +12,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(os.path.dirname(HERE), "vae2")
-OUT = os.path.join(PKG, "libvae2_hip.so")
-BUILD = os.path.join(HERE, "build")
+# A/B builds: VAE2_BUILD_TAG=t VAE2_DEFS="-DVAE2_ABLATE=1" -> libvae2_hip_t.so (own objects)
+TAG = os.environ.get("VAE2_BUILD_TAG", "")
+DEFS = os.environ.get("VAE2_DEFS", "").split()
+OUT = os.path.join(PKG, f"libvae2_hip_{TAG}.so" if TAG else "libvae2_hip.so")
+BUILD = os.path.join(HERE, f"build_{TAG}" if TAG else "build")
 SOURCES = ["conv.hip", "bn.hip", "resample.hip", "elbo.hip", "heads.hip", "clips.hip",
            "metrics.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "vae2_hip.h")]
@@ -61,7 +64,7 @@ def _compile(unit):
     deps = [os.path.join(HERE, src)] + [os.path.join(HERE, h) for h in HEADERS]
     if not _newer(obj, deps):
         return obj, None
-    cmd = [hipcc()] + FLAGS + EXTRA.get(src, []) + defs + ["-c", os.path.join(HERE, src), "-o", obj]
+    cmd = [hipcc()] + FLAGS + EXTRA.get(src, []) + defs + DEFS + ["-c", os.path.join(HERE, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"

@@ -27,7 +27,8 @@
 #include "common.h"
 
 // Diagnostic builds only (never the shipped library): -DVAE2_ABLATE=1 stages zeros
-// instead of loading the direct kernel's halo tile, =2 drops its output stores.
+// instead of loading the direct kernel's halo tile, 2 drops its output stores, 4 skips its
+// MFMA main loop (bits combine).
 #ifndef VAE2_ABLATE
 #define VAE2_ABLATE 0
 #endif
@@ -988,7 +989,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     };
     if (!BF) {
       load(fa0, fb0);
-      for (int ch = 0; ch < nch; ch += 2) {
+      for (int ch = 0; ch < ((VAE2_ABLATE & 4) ? 0 : nch); ch += 2) {
         load(fa1, fb1);
         mma(fa0, fb0);
         rem(fa0);
@@ -1130,7 +1131,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
         }
         if (n + 3 < p.n) {
           if (p.beta != 0.f) v += p.beta * (PFA ? yold[PFA ? i : 0][j] : yrt[PFA ? 0 : j]);
-          *reinterpret_cast<f4*>(yrow + n) = v;
+          if (!(VAE2_ABLATE & 2) || v[0] == 1234.5f) *reinterpret_cast<f4*>(yrow + n) = v;
         } else {
 #pragma unroll
           for (int q = 0; q < 4; ++q)

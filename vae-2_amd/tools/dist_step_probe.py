@@ -23,7 +23,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--graph", action="store_true", help="capture the step and replay it")
+    ap.add_argument("--capture-mode", default="global", choices=("global", "thread_local", "relaxed"))
+    ap.add_argument("--dump-after", type=float, default=0,
+                    help="print every thread's Python stack every N s (hang diagnosis)")
     a = ap.parse_args()
+    if a.dump_after > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(a.dump_after, repeat=True, exit=False)
     from helpers import build, make_cfg
     from vae2 import dist as vdist
     from vae2.model import FullModel_encdec
@@ -35,35 +41,52 @@ def main():
     vdist.FORCE = True
     vdist.set_sync_bn(True)
     hw, B = (64, 128), 2
-    ed, ez = build(make_cfg("w18", hw=hw))
-    fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).cuda()
-    fm.train()
-    fm.defer_checks = True
-    opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-3)
     g = torch.Generator().manual_seed(7)
     xs = [torch.randn(B, 9, *hw, generator=g).cuda() for _ in range(3)]
     eps = torch.randn(B, 10, 1, 1, generator=g).cuda()
     code = torch.randn(B, 10, 1, 1, generator=g).cuda()
 
-    def step():
-        opt.zero_grad()
-        fm.set_noise(eps, code)
-        loss = fm(*xs, 1.0)[0][0]
-        loss.backward()
-        vdist.allreduce_grads(opt.flats)
-        opt.step()
-        return loss
+    def make():
+        ed, ez = build(make_cfg("w18", hw=hw))
+        fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).cuda()
+        fm.train()
+        fm.defer_checks = True
+        opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-3)
 
-    run = step
+        def step():
+            opt.zero_grad()
+            fm.set_noise(eps, code)
+            loss = fm(*xs, 1.0)[0][0]
+            loss.backward()
+            vdist.allreduce_grads(opt.flats)
+            opt.step()
+            return loss
+        return step
+
+    warm = 2
+    ref = []
+    if a.graph:  # eager reference: the warm-up steps + the replayed ones
+        step = make()
+        for i in range(warm + a.steps):
+            ref.append(float(step()))
+        print("eager", [round(v, 4) for v in ref], flush=True)
+    run = make()
     if a.graph:
         from vae2.graph import StepGraph
         print("capturing", flush=True)
-        run = StepGraph(step, warmup=2).replay
+        run = StepGraph(run, warmup=warm, capture_error_mode=a.capture_mode).replay
+        print("captured", flush=True)
+    same = True
     for i in range(a.steps):
         t0 = time.time()
         loss = float(run())
         torch.cuda.synchronize()
-        print(f"step {i}: loss {loss:.4f} ({time.time() - t0:.2f} s)", flush=True)
+        if ref:
+            same &= loss == ref[warm + i]
+        print(f"step {i}: loss {loss:.6f} ({time.time() - t0:.2f} s)"
+              + (f" eager {ref[warm + i]:.6f}" if ref else ""), flush=True)
+    if ref:
+        print("graph == eager:", same, flush=True)
     dist.destroy_process_group()
     print("probe ok", flush=True)
 

@@ -156,7 +156,13 @@ class _Anchor(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, flat, lo, hi):
         ctx.args = (flat, lo, hi)
-        return x.view_as(x)
+        ctx.set_materialize_grads(False)  # gx is None when x's consumers skip it
+        out = x.view_as(x)
+        if not x.requires_grad:
+            # the output requires grad only through the anchor: its consumers (the
+            # posterior net's stem conv) compute no data gradient for it (ops._conv_bwd)
+            out._vae2_no_dx = True
+        return out
 
     @staticmethod
     def backward(ctx, gx, *_):
@@ -190,12 +196,16 @@ def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
     pending = []
     for f in flats:
         g = f.grad
-        done = sorted(_EARLY.pop(id(f), []))
+        done = sorted(_EARLY.pop(id(f), []), key=lambda e: (e[0], e[1]))
         works, gaps, pos = [], [], 0
         for lo, hi, w in done:  # the ranges no hook started yet
+            if lo < pos:  # a range reduced twice would be scaled by the world size
+                raise RuntimeError(f"overlapping early gradient buckets [{lo}, {hi}) "
+                                   f"(previous range ends at {pos}): a second backward "
+                                   "before allreduce_grads?")
             if lo > pos:
                 gaps.append((pos, lo))
-            pos = max(pos, hi)
+            pos = hi
             works += w
         if pos < g.numel():
             gaps.append((pos, g.numel()))
@@ -211,6 +221,43 @@ def allreduce_grads(flats, bucket_elems=BUCKET_ELEMS):
         for w in works:
             w.wait()  # the compute stream waits for the bucket (no host sync)
         call("vae2_scale", ops.ptr(g), ops.ptr(g), g.numel(), 1.0 / ws, ops.stream_ptr())
+
+
+_DDP_GUARD = False
+
+
+def guard_ddp():
+    """Make torch.nn.parallel.DistributedDataParallel refuse the HIP-path modules.
+
+    The reference wraps FullModel_encdec / FullModel_D in DDP(find_unused_parameters=True)
+    (/root/reference/tools/train.py:225-229).  Here the HIP backward kernels accumulate
+    every parameter gradient into the flat main_grad buffers (vae2.params), so DDP's
+    per-parameter gradient hooks never fire: it would all-reduce nothing and every rank
+    would silently train on its own gradients.  Wrapping a module that contains a HIP-path
+    network therefore raises, naming the replacement (allreduce_grads after backward).
+    Installed once, on import of vae2.hrnet; other modules wrap as before."""
+    global _DDP_GUARD
+    if _DDP_GUARD:
+        return
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    orig = DDP.__init__
+
+    def __init__(self, module, *args, **kwargs):
+        hip = [type(m).__name__ for m in module.modules() if getattr(m, "_vae2_hip_module", False)]
+        if hip:
+            raise RuntimeError(
+                f"DistributedDataParallel cannot wrap a HIP-path module ({hip[0]}): its "
+                "parameter gradients are accumulated into flat main_grad buffers, so DDP's "
+                "per-parameter hooks would never fire and no gradient would be all-reduced. "
+                "Call vae2.dist.set_sync_bn(True) once and vae2.dist.allreduce_grads("
+                "optimizer.flats) after backward() instead (INTEGRATION.md, 'The "
+                "reference's own tools/train.py').")
+        orig(self, module, *args, **kwargs)
+
+    __init__.__wrapped__ = orig
+    __init__.__doc__ = orig.__doc__
+    DDP.__init__ = __init__
+    _DDP_GUARD = True
 
 
 def reduce_tensor(inp):

@@ -20,7 +20,7 @@ from . import streams
 
 
 class StepGraph:
-    def __init__(self, step_fn, warmup=2):
+    def __init__(self, step_fn, warmup=2, capture_error_mode="global"):
         self.step_fn = step_fn
         dev = torch.cuda.current_device()
         side = torch.cuda.Stream(device=dev)
@@ -34,7 +34,7 @@ class StepGraph:
         self.graph = torch.cuda.CUDAGraph()
         streams._FORKED.clear()
         try:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
                 self.out = step_fn()
                 streams.join_all()
         finally:

@@ -29,6 +29,7 @@ from . import dist as vdist
 from . import ops, streams
 
 BN_MOMENTUM = 0.01
+vdist.guard_ddp()  # DDP around these networks would silently skip the gradient all-reduce
 logger = logging.getLogger(__name__)
 
 
@@ -373,6 +374,8 @@ def _ch_list(cfg):
 class HighResolutionNet(nn.Module):
     """Shared trunk: stem, layer1, stages 2-4, transitions, optional code-map
     transition and three heads (enc_hrnet.py:259-370)."""
+
+    _vae2_hip_module = True  # gradients go to main_grad (vae2.dist.guard_ddp)
 
     def __init__(self, config, **kwargs):
         extra = config.MODEL.EXTRA

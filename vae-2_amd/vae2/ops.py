@@ -510,7 +510,9 @@ class _defer_off:
 
 def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, group=None):
     """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b).  With a
-    ConvGroup the data gradient is queued on it (dx is complete once it is flushed)."""
+    ConvGroup the data gradient is queued on it (dx is complete once it is flushed).  An
+    input marked `_vae2_no_dx` (vae2.dist.anchor_reduce's output when its source needs no
+    gradient) gets none: it requires grad only to route the anchor's backward."""
     s = stream_ptr()
     xp, xa = act_of(x)
     dyp, dya = act_of(dy)
@@ -538,7 +540,7 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         if _WGRAD_BATCH[0] and not now:  # the deferred reduction reads it at the flush
             _WS_HOLD.append((torch.cuda.current_stream().cuda_stream, ws))
     dx = None
-    if need_dx:
+    if need_dx and not getattr(x, "_vae2_no_dx", False):
         link = spec.x_link
         beta = 0.0
         if link is not None and link.buf is not None:
