@@ -13,10 +13,10 @@ clips at 8 GPUs), fp32, random-init weights (seed 0, the reference's init),
 synthetic Gaussian clips resident in HBM.  One step = posterior net +
 reparameterisation + encoder + 2 decoders forward, L1 x3 + KL, backward, RCCL
 gradient all-reduce (N > 1, SyncBN statistics), Adam.  frames/s = clips * 9 /
-step time, whole job.  At N=1 the step is captured once as a HIP graph
-(vae2.graph.StepGraph: same kernels, one launch, bit-identical to eager steps —
-tests/test_graph_gpu.py) and replayed; the noise is drawn on the device inside the
-step so every replay samples fresh noise.
+step time, whole job.  The step is captured once as a HIP graph (vae2.graph.StepGraph:
+same kernels, one launch, bit-identical to eager steps -- tests/test_graph_gpu.py; at
+N > 1 with the RCCL collectives inside, tests/test_dist_rccl_gpu.py) and replayed; the
+noise is drawn on the device inside the step so every replay samples fresh noise.
 
 Printed JSON also carries:
   roofline      the dominant kernel by time (one instantiation, as rocprofv3 names
@@ -96,10 +96,12 @@ def parse():
                          "GAN_LAMBDA 1 (both LSGAN generator terms through the two "
                          "discriminators) + the discriminator step with its own Adam")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="replay the step as one captured HIP graph (auto: at N=1; the "
-                         "distributed step under capture is not enabled, DESIGN.md (e)).  The "
-                         "eager step measured 0-3%% faster on an idle host but 10-20%% "
-                         "slower when the host CPUs are busy; the graph replay is stable")
+                    help="replay the step as one captured HIP graph (auto = on, at every world "
+                         "size: the distributed step's RCCL collectives are captured in "
+                         "thread-local capture mode, vae2/graph.py; bit-identical to eager "
+                         "steps, tests/test_dist_rccl_gpu.py).  The eager step measured 0-3%% "
+                         "faster on an idle host but 10-20%% slower when the host CPUs are "
+                         "busy; the graph replay is stable")
     return ap.parse_args()
 
 
@@ -306,7 +308,7 @@ def main():
             opt_d.step()
         return losses[0]
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    use_graph = args.graph in ("on", "auto")
     step = eager_step
     if use_graph:
         from vae2.graph import StepGraph

@@ -132,3 +132,91 @@ def test_rccl_world1_dist_path_equals_single_process_step():
         assert grad_same, grad_rel
     assert grad_rel < 1e-5, grad_rel
 
+
+
+def _graph_work(port, q):
+    """World-1 RCCL group, distributed paths forced on: 2 warm-up + 3 eager steps of a
+    fresh model, then a fresh model captured as one HIP graph (vae2.graph.StepGraph,
+    thread-local capture: the RCCL watchdog thread queries events while the capture is
+    open) and replayed 3 times.  Losses and final parameters must be bit-identical."""
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from helpers import build, golden, make_cfg, t
+    from vae2 import dist as vdist
+    from vae2.graph import StepGraph
+    from vae2.model import FullModel_encdec
+    from vae2.optim import FusedAdam
+    torch.cuda.set_device(0)
+    g = golden("tiny_native")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    vdist.FORCE = True
+    vdist.set_sync_bn(True)
+    xs = [t(g[k]).cuda() for k in ("xt", "x2t", "x3t")]
+    eps, code = t(g["eps"]).cuda(), t(g["code"]).cuda()
+
+    def make():
+        ed, ez = build(make_cfg("tiny"))
+        fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).cuda()
+        fm.train()
+        fm.defer_checks = True
+        opt = FusedAdam([fm.encz_model, fm.encdec_model], lr=1e-3)
+
+        def step():
+            opt.zero_grad()
+            fm.set_noise(eps, code)
+            loss = fm(*xs, 1.0)[0][0]
+            loss.backward()
+            vdist.allreduce_grads(opt.flats)
+            opt.step()
+            return loss
+        return step, opt
+
+    step, opt = make()
+    eager = [float(step()) for _ in range(5)]
+    torch.cuda.synchronize()
+    p_eager = torch.cat([f.data for f in opt.flats]).cpu()
+    step, opt = make()
+    graph = StepGraph(step, warmup=2)
+    replay = []
+    for _ in range(3):
+        replay.append(float(graph.replay()))
+    torch.cuda.synchronize()
+    p_graph = torch.cat([f.data for f in opt.flats]).cpu()
+    q.put(("ok", eager, replay, bool(torch.equal(p_eager, p_graph)),
+           float((p_eager - p_graph).abs().max())))
+    dist.destroy_process_group()
+
+
+def _graph_worker(port, q):
+    try:
+        _graph_work(port, q)
+    except BaseException:
+        import traceback
+        q.put(("error", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.timeout(300)
+def test_rccl_world1_graph_capture_equals_eager():
+    """The distributed step (SyncBN exchanges, early and final gradient buckets as RCCL
+    collectives) captured as a HIP graph replays bit-identically to eager steps.  Bounded:
+    a hang in the capture fails the test instead of stalling the box."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_worker, args=(_port(), q))
+    p.start()
+    import queue
+    try:
+        res = q.get(timeout=200)
+    except queue.Empty:
+        p.kill()
+        pytest.fail(f"captured RCCL step did not report (exit code {p.exitcode})")
+    p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, eager, replay, same, maxdiff = res
+    print(f"eager {eager}, replay {replay}, params identical {same} (max |diff| {maxdiff:.3g})")
+    assert replay == eager[2:], (replay, eager)
+    assert same, maxdiff

@@ -159,6 +159,14 @@ int adj3_fuse_launch(const float* dy, const vae2_act* dyd, int n, float* const* 
                      const vae2_act* dxds, const float* betas, hipStream_t st);
 extern int g_relu_dual_q;  // heads.hip: vae2_heads_set_algo bit 7 clears it
 
+// Internal (wgrad_narrow.hip): the narrow-channel 3x3 weight gradient.  _splits: partial
+// slabs it writes for this layer (0: not handled); _launch: writes them into part
+// ([splits][cout][9 * cin4]) and returns their number, 0 when not handled, < 0 on error.
+int64_t wgrad3n_splits(const vae2_act* xd, const vae2_act* dyd);
+int wgrad3n_launch(const float* x, const vae2_act* xd, const float* dy, const vae2_act* dyd,
+                   float* part, const float* isave, int irelu, uint32_t x_bytes,
+                   uint32_t dy_bytes, hipStream_t s);
+
 // Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,
                             float* dbias, int accumulate, void* stream);

@@ -1341,10 +1341,12 @@ int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients ov
 int g_gemm1_tn = 4;
 int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 16 * TM pixels (1, 2)
 int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
+int g_wgrad_narrow = 1;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
+                          // (0 off, 1 on, 2 on with register prefetch)
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
-    g_gemm1_tm, g_igemm_nr;
+    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2756,6 +2758,11 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_igemm_nr = value ? 1 : 0;
     return prev;
   }
+  if (key == 7) {
+    const int prev = g_wgrad_narrow;
+    g_wgrad_narrow = value >= 0 && value <= 2 ? value : 1;
+    return prev;
+  }
   return -1;
 }
 
@@ -3153,6 +3160,8 @@ int64_t vae2_conv2d_bwd_weight_ws_size(const vae2_act* xd, const vae2_act* dyd, 
     W3Tile t3 = pick_w3tile(xd, dyd, k);
     const int64_t part3 = (int64_t)t3.splits * dyd->c * ncol4;
     if (part3 > part) part = part3;
+    const int64_t partn = wgrad3n_splits(xd, dyd) * dyd->c * ncol4;
+    if (partn > part) part = partn;
   }
   int64_t bias_part = 2 * vae2_bn_partial_rows(dyd) * dyd->c;
   return part + bias_part + 4;
@@ -3176,7 +3185,11 @@ static int bwd_weight_impl(const float* x, const vae2_act* xd, const float* dy,
                       vec_ok(x, (int)xd->ps) && vec_ok(dy, (int)dyd->ps);
   VAE2_REQUIRE(direct || !isave, fn,
                "input BatchNorm needs the direct 3x3 weight-gradient kernel (vae2_conv2d_bnin_ok)");
-  if (direct) {
+  if (direct && k == 3) {  // the 18 / 36 / 72-channel branches (wgrad_narrow.hip)
+    splits = wgrad3n_launch(x, xd, dy, dyd, ws, isave, irelu, act_bytes(xd), act_bytes(dyd), s);
+    if (splits < 0) return check_launch(fn);
+  }
+  if (direct && !splits) {
     W3Tile t3 = pick_w3tile(xd, dyd, k);
     WGrad3 q{};
     q.x = x; q.x_ps = (int)xd->ps; q.cin = (int)xd->c; q.cin4 = cin4;

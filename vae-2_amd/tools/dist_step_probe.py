@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--graph", action="store_true", help="capture the step and replay it")
-    ap.add_argument("--capture-mode", default="global", choices=("global", "thread_local", "relaxed"))
+    ap.add_argument("--capture-mode", default=None, choices=("global", "thread_local", "relaxed"))
     ap.add_argument("--dump-after", type=float, default=0,
                     help="print every thread's Python stack every N s (hang diagnosis)")
     a = ap.parse_args()

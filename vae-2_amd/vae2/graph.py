@@ -13,15 +13,32 @@ tests/test_graph_gpu.py checks bit-identical parameters after several steps.
 Inputs the step reads (clips, noise) must live in static device tensors that
 the caller refills before replay (or draws inside the step with device RNG,
 which CUDAGraph advances per replay).
+
+Distributed steps (RCCL collectives inside the graph): the capture runs in
+thread-local capture mode.  ProcessGroupNCCL's watchdog thread polls the events of
+earlier (eager, warm-up) collectives with hipEventQuery; under the default global
+mode HIP refuses that call from any thread while a capture is open
+(hipErrorStreamCaptureUnsupported), the watchdog thread dies and aborts the process
+(observed on MI355X with a world-size-1 RCCL group; round 4 saw the same capture
+hang).  Thread-local mode restricts only the capturing thread.
 """
 import torch
+import torch.distributed as dist
 
 from . import streams
 
 
+def _default_capture_mode():
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        return "thread_local"  # the RCCL watchdog thread queries events during the capture
+    return "global"
+
+
 class StepGraph:
-    def __init__(self, step_fn, warmup=2, capture_error_mode="global"):
+    def __init__(self, step_fn, warmup=2, capture_error_mode=None):
         self.step_fn = step_fn
+        if capture_error_mode is None:
+            capture_error_mode = _default_capture_mode()
         dev = torch.cuda.current_device()
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream())
