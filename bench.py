@@ -91,6 +91,9 @@ def parse():
                     help="vae2_conv2d_set_tune key=value[,key=value] (launch-shape A/B)")
     ap.add_argument("--side-streams", choices=("on", "off"), default="on",
                     help="posterior net / past decoder on side HIP streams (A/B)")
+    ap.add_argument("--syncbn-exchange", choices=("ipc", "rccl"), default="ipc",
+                    help="N > 1: the SyncBN statistics through the one-shot IPC peer all-reduce "
+                         "kernel (vae2_syncbn_allreduce) or RCCL all_reduce")
     ap.add_argument("--full-step", action="store_true",
                     help="the reference's full training iteration (function.py:443-512): "
                          "GAN_LAMBDA 1 (both LSGAN generator terms through the two "
@@ -240,6 +243,8 @@ def main():
     from vae2.optim import FusedAdam
     config = load_config(args)
     vdist.set_sync_bn(config.MI355X.SYNC_BN)
+    if world > 1 and config.MI355X.SYNC_BN and args.syncbn_exchange == "ipc":
+        vdist.init_syncbn_ipc()  # one-shot peer all-reduce (RCCL stays if it does not come up)
     if args.side_streams == "off":
         from vae2 import streams as vstreams
         vstreams.ENABLED = False
@@ -318,6 +323,7 @@ def main():
         step()
     torch.cuda.synchronize()
     fm.check_anomalies()
+    vdist.syncbn_check()  # (IPC SyncBN exchange: no timed-out exchange)
 
     # ---- timed region: the metric (full stream concurrency, no instrumentation) ----
     if world > 1:
@@ -335,6 +341,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     fm.check_anomalies()
+    vdist.syncbn_check()
     last_loss = float(loss.detach())
 
     # ---- profiled phase: the same step eager, every C-ABI call timed with HIP events
@@ -369,6 +376,7 @@ def main():
                        "global_batch": world * B, "frames_per_clip": 3 * L,
                        "image": [H, W], "parallelism": f"dp{world}",
                        "sync_bn": world > 1 and config.MI355X.SYNC_BN,
+                       "sync_bn_exchange": vdist.syncbn_exchange() if world > 1 else None,
                        "launch": "hip_graph" if use_graph else "eager",
                        "mfma_operands": ("bf16 (RNE; fp32 accumulation, fp32 activations in "
                                          "HBM, fp32 BN / loss / Adam)" if args.dtype == "bf16"

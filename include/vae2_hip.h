@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 10
+#define VAE2_ABI_VERSION 11
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -633,6 +633,29 @@ int vae2_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n,
 /* dst = src * scale, for fp32 buffers (grad averaging after all-reduce).       */
 int vae2_scale(float* dst, const float* src, int64_t n, float scale,
                void* stream);
+
+/* ------------------------------------------------------ SyncBN exchange ---- */
+
+/* ABI 11: one-shot peer all-reduce of the SyncBatchNorm statistics between the ranks of
+ * one node (replaces the per-layer SyncBatchNorm all-reduces of the reference's DDP setup,
+ * tools/train.py:216-218; vae2/dist.py makes one exchange per BN depth level).  Every rank
+ * stores its payload into a slot of every rank's receive area (IPC-mapped device memory,
+ * xGMI), raises its arrival flag there, waits for all flags of its own area and sums the
+ * world payloads in rank order: identical doubles on every rank, one kernel per exchange.
+ * Setup (collective): vae2_syncbn_comm_init allocates and zeroes this rank's area
+ * (vae2_syncbn_comm_bytes) and writes its 64-byte IPC handle; the handles of all ranks,
+ * concatenated in rank order, go to vae2_syncbn_comm_connect.  n <= max_elems doubles
+ * per call; the calls are stream-ordered and must be made in the same order on every
+ * rank (a HIP graph may capture them).  Waits are bounded (60 s): a missing peer sets the
+ * error word (vae2_syncbn_comm_error, a synchronous read) instead of hanging.  world <= 8. */
+typedef struct vae2_syncbn_comm vae2_syncbn_comm;
+int64_t vae2_syncbn_comm_bytes(int world, int64_t max_elems);
+int vae2_syncbn_comm_init(int rank, int world, int64_t max_elems, void* handle_out,
+                          vae2_syncbn_comm** out);
+int vae2_syncbn_comm_connect(vae2_syncbn_comm* comm, const void* handles);
+int vae2_syncbn_allreduce(vae2_syncbn_comm* comm, double* buf, int64_t n, void* stream);
+int vae2_syncbn_comm_error(vae2_syncbn_comm* comm, int64_t* host_out);
+int vae2_syncbn_comm_destroy(vae2_syncbn_comm* comm);
 
 #ifdef __cplusplus
 }

@@ -144,7 +144,7 @@ def _w18_inputs():
     return xs, eps, code
 
 
-def _w18_work(rank, world, port, q):
+def _w18_work(rank, world, port, q, ipc=False):
     import sys
     for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -156,14 +156,20 @@ def _w18_work(rank, world, port, q):
     from vae2.model import FullModel_encdec
     from vae2.optim import FusedAdam
     dev = "cuda:0"
+    torch.cuda.set_device(0)
     vdist.set_sync_bn(True)
     calls = [0]
     orig = vdist.all_reduce_
+    orig_sb = vdist.syncbn_all_reduce_
+    if ipc:  # the one-shot IPC exchange (csrc/syncbn.hip) carries the SyncBN statistics
+        vdist.FORCE_IPC = True
+        assert vdist.init_syncbn_ipc(), "IPC SyncBN exchange did not come up"
+        assert vdist.syncbn_exchange() == "ipc"
 
     def counting(t_, group=None):
         calls[0] += 1
-        return orig(t_, group=group)
-    vdist.all_reduce_ = counting
+        return orig_sb(t_, group=group)
+    vdist.syncbn_all_reduce_ = counting
     kw = dict(arch="w18", hw=W18_HW)
     ed, ez = build(make_cfg(**kw))
     fm = FullModel_encdec(ez, ed, None, None, None, None, None, 1.0, 0.1, 1.0, 0.0).to(dev)
@@ -179,7 +185,8 @@ def _w18_work(rank, world, port, q):
     exchanges = calls[0]
     vdist.allreduce_grads(opt.flats)
     torch.cuda.synchronize()
-    vdist.all_reduce_ = orig
+    vdist.syncbn_all_reduce_ = orig_sb
+    vdist.syncbn_check()
     loss = losses[0].detach().clone()
     orig(loss)
     gsum = float(torch.cat([f.grad for f in opt.flats]).double().sum())
@@ -196,9 +203,9 @@ def _w18_work(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _w18_worker(rank, world, port, q):
+def _w18_worker(rank, world, port, q, ipc=False):
     try:
-        _w18_work(rank, world, port, q)
+        _w18_work(rank, world, port, q, ipc)
     except BaseException:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
@@ -206,8 +213,10 @@ def _w18_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(600)
-def test_two_ranks_w18_sync_bn_matches_oracle():
-    """2 ranks x 1 clip (SyncBN exchanges per depth level over gloo, gradient mean) equal
+@pytest.mark.parametrize("ipc", [False, True])
+def test_two_ranks_w18_sync_bn_matches_oracle(ipc):
+    """2 ranks x 1 clip (SyncBN exchanges per depth level over gloo -- or, ipc, through the
+    one-shot IPC peer all-reduce kernel vae2_syncbn_allreduce -- gradient mean) equal
     the oracle's 1 rank x 2 clips: the mean loss within 1e-5, x2t_hat within 1e-4 and the
     decoder frames within 1e-3, every averaged parameter gradient against
     the fp64 oracle with the calibrated rule of test_model_gpu (fp32 oracle distance and
@@ -219,7 +228,7 @@ def test_two_ranks_w18_sync_bn_matches_oracle():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_w18_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_w18_worker, args=(r, 2, port, q, ipc)) for r in range(2)]
     for p in procs:
         p.start()
     import queue

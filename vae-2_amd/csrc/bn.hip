@@ -8,6 +8,8 @@
 // of per-channel fp32 sums per block (fixed pixel ranges), then one block per
 // channel sums the rows in double in a fixed tree order.  With SyncBN the double
 // sums are what crosses ranks.
+#include <algorithm>
+
 #include "common.h"
 
 namespace vae2 {
@@ -596,7 +598,11 @@ struct BnLayer {
 struct BnMulti {
   BnLayer L[kBnMaxLayers];
   int n;
+  int v2;  // buffer-resource bodies (every extent < 2 GB; vae2_conv2d_set_tune key 8)
 };
+
+// vae2_conv2d_set_tune key 8: 0 = the round-4 pointer-arithmetic BatchNorm bodies (A/B)
+int g_bn_v2 = 1;
 
 __device__ __forceinline__ int bn_layer_of(const BnMulti& m, int b) {
   int i = 0;
@@ -654,7 +660,80 @@ __device__ __forceinline__ void bn_apply_body(const BnLayer& L, int blk) {
   }
 }
 
+// Buffer-resource form of bn_apply_body (same arithmetic; see bn_bwd_apply_body2).
+__device__ __forceinline__ void bn_apply_body2(const BnLayer& L, int blk) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= L.rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const int nv = C - c < 4 ? C - c : 4;
+  const bool part = (C & 3) != 0;
+  const uint32_t P = (uint32_t)L.P;
+  const uint32_t cb = (uint32_t)C * 4u;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(L.save, 4u * cb);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(L.x, P * (uint32_t)L.x_ps * 4u);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(L.o, P * (uint32_t)L.o_ps * 4u);
+  const uint32_t pb = (uint32_t)blk * (uint32_t)(L.rows * kApplyU) + (uint32_t)r;
+  uint32_t pp[kApplyU];
+  bool in[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const uint32_t p = pb + (uint32_t)(u * L.rows);
+    in[u] = p < P;
+    pp[u] = in[u] ? p : P - 1;
+  }
+  f4 v[kApplyU], rv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) v[u] = load4(rx, (pp[u] * (uint32_t)L.x_ps + (uint32_t)c) * 4u);
+  if (L.a) {
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(L.a, P * (uint32_t)L.a_ps * 4u);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) rv[u] = load4(ra, (pp[u] * (uint32_t)L.a_ps + (uint32_t)c) * 4u);
+  } else if (L.rx) {
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(L.rx, P * (uint32_t)L.rx_ps * 4u);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) rv[u] = load4(rr, (pp[u] * (uint32_t)L.rx_ps + (uint32_t)c) * 4u);
+  }
+  auto last_row4 = [&](__amdgpu_buffer_rsrc_t rr, uint32_t row) {
+    f4 t;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = load1(rr, row + 4u * (uint32_t)(c + k < C ? c + k : C - 1));
+    return t;
+  };
+  const f4 sc = load4(rs, 2u * cb + 4u * (uint32_t)c), sh = last_row4(rs, 3u * cb);
+  f4 rsc = {0.f, 0.f, 0.f, 0.f}, rsh = rsc;
+  if (L.rx) {
+    const __amdgpu_buffer_rsrc_t rrs = make_rsrc(L.rsave, 4u * cb);
+    rsc = load4(rrs, 2u * cb + 4u * (uint32_t)c);
+    rsh = last_row4(rrs, 3u * cb);
+  }
+  const __amdgpu_buffer_rsrc_t rm = make_rsrc(L.mk, L.mk ? P * (uint32_t)c4 : 0u);
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    f4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float t = __builtin_fmaf(v[u][k], sc[k], sh[k]);
+      if (L.a) t += rv[u][k];
+      else if (L.rx) t += __builtin_fmaf(rv[u][k], rsc[k], rsh[k]);
+      o[k] = (L.relu && t < 0.f) ? 0.f : t;  // NaN propagates (torch.relu)
+    }
+    const uint32_t off = in[u] ? (pp[u] * (uint32_t)L.o_ps + (uint32_t)c) * 4u : kOOB;
+    if (part) store_quad(ro, off, o, nv);
+    else store4(ro, off, o);
+    if (L.mk)  // threshold_backward's test (y > 0: NaN and 0 cut the gradient)
+      __builtin_amdgcn_raw_buffer_store_b8(
+          (uint8_t)((o[0] > 0.f) | ((o[1] > 0.f) << 1) | ((o[2] > 0.f) << 2) | ((o[3] > 0.f) << 3)),
+          rm, in[u] ? pp[u] * (uint32_t)c4 + (uint32_t)(c >> 2) : kOOB, 0, 0);
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_apply_multi_kernel(BnMulti m) {
+  const int i = bn_layer_of(m, blockIdx.x);
+  bn_apply_body2(m.L[i], blockIdx.x - m.L[i].blk0);
+}
+
+__global__ __launch_bounds__(256) void bn_apply_multi_r4_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
   bn_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
 }
@@ -751,8 +830,114 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
   }
 }
 
+// Buffer-resource form of bn_bwd_reduce_body (same arithmetic and summation order).
+__device__ __forceinline__ void bn_bwd_reduce_body2(const BnLayer& L, int blk, int nblk,
+                                                   float* red0, float* red1) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  const int64_t p0 = blk * L.ppb;
+  int64_t p1 = p0 + L.ppb;
+  if (p1 > L.P) p1 = L.P;
+  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s0;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const uint8_t* mk = L.relu ? L.mk : nullptr;  // stored mask, else y, else from x
+  const float* y = L.relu && !mk ? L.a : nullptr;
+  const bool rb = L.rx != nullptr;  // + the residual BN's sum g * xhat_r (same g)
+  const uint32_t P = (uint32_t)L.P;
+  const __amdgpu_buffer_rsrc_t rxx = make_rsrc(L.x, P * (uint32_t)L.x_ps * 4u);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(L.dy, P * (uint32_t)L.dy_ps * 4u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, y ? P * (uint32_t)L.a_ps * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t rm = make_rsrc(mk, mk ? P * (uint32_t)c4 : 0u);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(L.rx, rb ? P * (uint32_t)L.rx_ps * 4u : 0u);
+  if (tid < L.rows * c4) {
+    const f4 mean = chan4(L.save, c, C), invstd = chan4(L.save + C, c, C);
+    const f4 sc = chan4(L.save + 2 * C, c, C), sh = chan4(L.save + 3 * C, c, C);
+    f4 rmean = s0, rinv = s0;
+    if (rb) { rmean = chan4(L.rsave, c, C); rinv = chan4(L.rsave + C, c, C); }
+    // kApplyU pixels' loads in flight per thread, then their math in pixel order (the
+    // same accumulation order as one pixel at a time)
+    for (int64_t pb = p0 + r; pb < p1; pb += (int64_t)kApplyU * L.rows) {
+      f4 xv[kApplyU], gv[kApplyU], yv[kApplyU], rv[kApplyU];
+      uint32_t mv[kApplyU];
+      // unconditional loads (pixels past p1 re-read p1 - 1, not summed), uniform branches
+      // outside the pixel loop: all pixels' loads in flight together
+      uint32_t pp[kApplyU];
+#pragma unroll
+      for (int u = 0; u < kApplyU; ++u)
+        pp[u] = (uint32_t)(pb + u * L.rows < p1 ? pb + u * L.rows : p1 - 1);
+#pragma unroll
+      for (int u = 0; u < kApplyU; ++u) {
+        xv[u] = load4(rxx, (pp[u] * (uint32_t)L.x_ps + (uint32_t)c) * 4u);
+        gv[u] = load4(rdy, (pp[u] * (uint32_t)L.dy_ps + (uint32_t)c) * 4u);
+      }
+      if (y) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) yv[u] = load4(ry, (pp[u] * (uint32_t)L.a_ps + (uint32_t)c) * 4u);
+      }
+      if (mk) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) mv[u] = load_u8(rm, pp[u] * (uint32_t)c4 + (uint32_t)(c >> 2));
+      }
+      if (rb) {
+#pragma unroll
+        for (int u = 0; u < kApplyU; ++u) rv[u] = load4(rr, (pp[u] * (uint32_t)L.rx_ps + (uint32_t)c) * 4u);
+      }
+#pragma unroll
+      for (int u = 0; u < kApplyU; ++u) {
+        if (pb + u * L.rows >= p1) break;
+        const f4 xa = xv[u];
+        f4 ga = gv[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (L.relu && !(mk ? ((mv[u] >> k) & 1u) != 0
+                             : (y ? yv[u][k] : __builtin_fmaf(xa[k], sc[k], sh[k])) > 0.f))
+            ga[k] = 0.f;
+          s0[k] += ga[k];
+          s1[k] += ga[k] * (xa[k] - mean[k]) * invstd[k];
+          if (rb) s2[k] += ga[k] * (rv[u][k] - rmean[k]) * rinv[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red0[r * 4 * c4 + c + k] = s0[k];
+      red1[r * 4 * c4 + c + k] = s1[k];
+    }
+  }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < L.rows; ++i) {
+      a += red0[i * 4 * c4 + ch];
+      b += red1[i * 4 * c4 + ch];
+    }
+    L.part[(int64_t)blk * C + ch] = a;
+    L.part[((int64_t)nblk + blk) * C + ch] = b;
+    if (rb) L.rpart[(int64_t)blk * C + ch] = a;  // the residual BN's sum g: the same sum
+  }
+  if (!rb) return;
+  __syncthreads();
+  if (tid < L.rows * c4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red1[r * 4 * c4 + c + k] = s2[k];
+  }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    float b = 0.f;
+    for (int i = 0; i < L.rows; ++i) b += red1[i * 4 * c4 + ch];
+    L.rpart[((int64_t)nblk + blk) * C + ch] = b;
+  }
+}
+
 // nblk of layer i = blk0[i+1] - blk0[i] (the last: gridDim.x - blk0)
 __global__ __launch_bounds__(256) void bn_bwd_reduce_multi_kernel(BnMulti m) {
+  __shared__ float red[2][256 * 4];
+  const int i = bn_layer_of(m, blockIdx.x);
+  const int nblk = (i + 1 < m.n ? m.L[i + 1].blk0 : (int)gridDim.x) - m.L[i].blk0;
+  bn_bwd_reduce_body2(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_multi_r4_kernel(BnMulti m) {
   __shared__ float red[2][256 * 4];
   const int i = bn_layer_of(m, blockIdx.x);
   const int nblk = (i + 1 < m.n ? m.L[i + 1].blk0 : (int)gridDim.x) - m.L[i].blk0;
@@ -849,7 +1034,154 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
   }
 }
 
+// Buffer-resource form of bn_bwd_apply_body (same arithmetic, element for element): 32-bit
+// byte offsets instead of 64-bit pointer math, 16-byte coefficient loads (out-of-range
+// lanes read 0), pixels past P clamped for the loads and dropped for the stores
+// (out-of-range offsets), partial channel quads stored by store_quad -- no per-lane
+// branches.  SQ PMC of the round-4 form on the 18 / 36 / 72-channel launches: 405 VALU +
+// 308 SALU instructions per wave (64-bit addresses, per-channel scalar coefficient loads,
+// exec-mask branches around the partial-quad stores), 40 % of wave cycles in issue stalls.
+// Every tensor extent < 2 GB (host check, bn_multi_launch).
+__device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
+  const int C = L.C, c4 = (C + 3) >> 2;
+  const int tid = threadIdx.x;
+  if (tid >= L.rows * c4) return;
+  const int r = tid / c4, c = 4 * (tid - r * c4);
+  const int nv = C - c < 4 ? C - c : 4;  // valid channels of this quad
+  const bool part = (C & 3) != 0;        // (uniform) some quad is partial
+  const uint32_t P = (uint32_t)L.P;
+  const bool relu = L.relu != 0;
+  const bool usemk = relu && L.mk != nullptr;
+  const bool usey = relu && !usemk && L.a != nullptr;
+  const bool rb = L.rx != nullptr;
+  const bool dres = L.dres != nullptr;
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(L.dy, P * (uint32_t)L.dy_ps * 4u);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(L.x, P * (uint32_t)L.x_ps * 4u);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(L.o, P * (uint32_t)L.o_ps * 4u);
+  const uint32_t pb = (uint32_t)blk * (uint32_t)(L.rows * kApplyU) + (uint32_t)r;
+  uint32_t pp[kApplyU];
+  bool in[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    const uint32_t p = pb + (uint32_t)(u * L.rows);
+    in[u] = p < P;
+    pp[u] = in[u] ? p : P - 1;
+  }
+  f4 gv[kApplyU], xv[kApplyU], yv[kApplyU], rxv[kApplyU], dv[kApplyU];
+  uint32_t mv[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    gv[u] = load4(rdy, (pp[u] * (uint32_t)L.dy_ps + (uint32_t)c) * 4u);
+    xv[u] = load4(rx, (pp[u] * (uint32_t)L.x_ps + (uint32_t)c) * 4u);
+  }
+  if (usey) {
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(L.a, P * (uint32_t)L.a_ps * 4u);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) yv[u] = load4(ry, (pp[u] * (uint32_t)L.a_ps + (uint32_t)c) * 4u);
+  }
+  if (usemk) {
+    const __amdgpu_buffer_rsrc_t rm = make_rsrc(L.mk, P * (uint32_t)c4);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) mv[u] = load_u8(rm, pp[u] * (uint32_t)c4 + (uint32_t)(c >> 2));
+  }
+  if (rb) {
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(L.rx, P * (uint32_t)L.rx_ps * 4u);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) rxv[u] = load4(rr, (pp[u] * (uint32_t)L.rx_ps + (uint32_t)c) * 4u);
+  }
+  const __amdgpu_buffer_rsrc_t rdr = make_rsrc(L.dres, dres ? P * (uint32_t)L.dres_ps * 4u : 0u);
+  if (dres && L.dres_acc) {
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) dv[u] = load4(rdr, (pp[u] * (uint32_t)L.dres_ps + (uint32_t)c) * 4u);
+  }
+  // per-channel coefficients: 16-byte loads of the quad where they stay inside the buffer
+  // (a partial quad then reads the next coefficient row: only its dropped lanes use those),
+  // per-channel loads of clamped channels for the last row of a buffer (a 16-byte load that
+  // crosses the end of the range returns 0 in every lane)
+  const uint32_t cb = (uint32_t)C * 4u, qb = (uint32_t)c * 4u;
+  auto last_row4 = [&](__amdgpu_buffer_rsrc_t rr, uint32_t row) {
+    f4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = load1(rr, row + 4u * (uint32_t)(c + k < C ? c + k : C - 1));
+    return v;
+  };
+  auto last_row_d4 = [&](__amdgpu_buffer_rsrc_t rr, uint32_t row, float scale) {
+    f4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t o = row + 8u * (uint32_t)(c + k < C ? c + k : C - 1);
+      const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(rr, o, 0, 0);
+      v[k] = (float)__builtin_bit_cast(double, b) * scale;
+    }
+    return v;
+  };
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(L.save, 4u * cb);
+  const f4 mean = load4(rs, qb), invstd = load4(rs, cb + qb);
+  const f4 sc = load4(rs, 2u * cb + qb), sh = last_row4(rs, 3u * cb);
+  const __amdgpu_buffer_rsrc_t rsum = make_rsrc(L.sums, 2u * cb * 2u);
+  const d2 s01 = load_d2(rsum, 2u * qb), s23 = load_d2(rsum, 2u * qb + 16u);
+  f4 gam = {1.f, 1.f, 1.f, 1.f};
+  if (L.gamma) gam = last_row4(make_rsrc(L.gamma, cb), 0u);
+  const double count = L.countp ? *L.countp : L.count;
+  const float inv_n = (float)(1.0 / count);
+  const f4 mg = {(float)s01[0] * inv_n, (float)s01[1] * inv_n, (float)s23[0] * inv_n, (float)s23[1] * inv_n};
+  const f4 mgx = last_row_d4(rsum, 2u * cb, inv_n);
+  const f4 k4 = gam * invstd;
+  f4 rmean = {0.f, 0.f, 0.f, 0.f}, rinv = rmean, rmg = rmean, rmgx = rmean, rk4 = rmean;
+  if (rb) {
+    const __amdgpu_buffer_rsrc_t rrs = make_rsrc(L.rsave, 4u * cb);
+    rmean = load4(rrs, qb);
+    rinv = load4(rrs, cb + qb);
+    const __amdgpu_buffer_rsrc_t rrsum = make_rsrc(L.rsums, 2u * cb * 2u);
+    const d2 a01 = load_d2(rrsum, 2u * qb), a23 = load_d2(rrsum, 2u * qb + 16u);
+    rmg = f4{(float)a01[0] * inv_n, (float)a01[1] * inv_n, (float)a23[0] * inv_n, (float)a23[1] * inv_n};
+    rmgx = last_row_d4(rrsum, 2u * cb, inv_n);
+    f4 rgam = {1.f, 1.f, 1.f, 1.f};
+    if (L.rgamma) rgam = last_row4(make_rsrc(L.rgamma, cb), 0u);
+    rk4 = rgam * rinv;
+  }
+  const __amdgpu_buffer_rsrc_t rrdx = make_rsrc(L.rdx, rb ? P * (uint32_t)L.rdx_ps * 4u : 0u);
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    f4 g = gv[u], o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bool pos;
+      if (usemk) pos = ((mv[u] >> k) & 1u) != 0;
+      else if (usey) pos = yv[u][k] > 0.f;
+      else pos = __builtin_fmaf(xv[u][k], sc[k], sh[k]) > 0.f;
+      if (relu && !pos) g[k] = 0.f;
+      const float xh = (xv[u][k] - mean[k]) * invstd[k];
+      o[k] = k4[k] * (g[k] - mg[k] - xh * mgx[k]);
+    }
+    const uint32_t po = in[u] ? pp[u] : 0x7fffffffu;  // pixels past P: dropped stores
+    auto off = [&](int ps) { return in[u] ? (po * (uint32_t)ps + (uint32_t)c) * 4u : kOOB; };
+    if (dres) {
+      const f4 dr = L.dres_acc ? g + dv[u] : g;
+      if (part) store_quad(rdr, off(L.dres_ps), dr, nv);
+      else store4(rdr, off(L.dres_ps), dr);
+    }
+    if (part) store_quad(ro, off(L.o_ps), o, nv);
+    else store4(ro, off(L.o_ps), o);
+    if (rb) {  // the residual BN's input gradient from the same g (bn_bwd_apply's formula)
+      f4 rdv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float xh = (rxv[u][k] - rmean[k]) * rinv[k];
+        rdv[k] = rk4[k] * (g[k] - rmg[k] - xh * rmgx[k]);
+      }
+      if (part) store_quad(rrdx, off(L.rdx_ps), rdv, nv);
+      else store4(rrdx, off(L.rdx_ps), rdv);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
+  const int i = bn_layer_of(m, blockIdx.x);
+  bn_bwd_apply_body2(m.L[i], blockIdx.x - m.L[i].blk0);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_multi_r4_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
   bn_bwd_apply_body(m.L[i], blockIdx.x - m.L[i].blk0);
 }
@@ -1242,13 +1574,27 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       }
     }
     if (blocks == 0) continue;
+    m.v2 = g_bn_v2;
+    for (int j = 0; j < m.n; ++j) {  // 32-bit buffer offsets: every extent below 2 GB
+      const vae2_bn_layer& l = ls[i0 + j];
+      const int64_t P = act_pixels(&l.xd);
+      const int64_t ext = P * std::max({l.xd.ps, l.od.ps, l.dyd.ps, l.ad.ps, l.dresd.ps,
+                                        l.rxd.ps, l.rdxd.ps, (int64_t)1}) * 4;
+      if (ext >= (int64_t(1) << 31)) m.v2 = 0;
+    }
     hipStream_t st = as_stream(stream);
-    if (kind == 0)
+    if (kind == 0 && m.v2)
       VAE2_LAUNCH(bn_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
-    else if (kind == 1)
+    else if (kind == 0)
+      VAE2_LAUNCH(bn_apply_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else if (kind == 1 && m.v2)
       VAE2_LAUNCH(bn_bwd_reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
-    else
+    else if (kind == 1)
+      VAE2_LAUNCH(bn_bwd_reduce_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else if (m.v2)
       VAE2_LAUNCH(bn_bwd_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+    else
+      VAE2_LAUNCH(bn_bwd_apply_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     const int rc = check_launch(fn);
     if (rc) return rc;
   }

@@ -18,7 +18,7 @@ DEFS = os.environ.get("VAE2_DEFS", "").split()
 OUT = os.path.join(PKG, f"libvae2_hip_{TAG}.so" if TAG else "libvae2_hip.so")
 BUILD = os.path.join(HERE, f"build_{TAG}" if TAG else "build")
 SOURCES = ["conv.hip", "bn.hip", "resample.hip", "elbo.hip", "heads.hip", "clips.hip",
-           "metrics.hip", "wgrad_narrow.hip"]
+           "metrics.hip", "wgrad_narrow.hip", "syncbn.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "vae2_hip.h")]
 ARCH = os.environ.get("VAE2_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

@@ -10,6 +10,8 @@
 
 namespace vae2 {
 
+constexpr int kSyncMaxRanks = 8;  // syncbn.hip: ranks of one node
+
 // ------------------------------------------------------------ errors ----
 void set_error(const std::string& msg);
 int fail(const char* fn, const std::string& msg);  // returns -22
@@ -66,6 +68,36 @@ __device__ __forceinline__ bf16x8 pack_bf16(f4 a, f4 b) {
 
 __device__ __forceinline__ void store1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, uint32_t off, f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t load_u8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+
+__device__ __forceinline__ d2 load_d2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// The first n (1..4) channels of a channel quad at byte offset off, without branches: a
+// whole quad as one 16-byte store, a partial one as (2 +) 1 stores; the unused forms get an
+// out-of-range offset (dropped).  Channels past n are never written (they may belong to
+// the next tensor of a concatenation buffer).
+__device__ __forceinline__ void store_quad(__amdgpu_buffer_rsrc_t r, uint32_t off, f4 v, int n) {
+  store4(r, n >= 4 ? off : kOOB, v);
+  // (the pair as a shuffle of the bit-cast quad: an element-wise {v[0], v[1]} initializer
+  //  was compiled to {v[0], v[0]} by hipcc 7.2 here -- channel 1 of every partial quad lost)
+  const u32x4 w = __builtin_bit_cast(u32x4, v);
+  const u32x2 lo = __builtin_shufflevector(w, w, 0, 1);
+  __builtin_amdgcn_raw_buffer_store_b64(lo, r, (n & 2) && n < 4 ? off : kOOB, 0, 0);
+  store1(r, (n & 1) ? off + 4u * (uint32_t)(n & 2) : kOOB, (n & 2) ? v[2] : v[0]);
 }
 
 // ------------------------------------------------------- activations ----

@@ -1343,6 +1343,7 @@ int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 1
 int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
 int g_wgrad_narrow = 1;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
                           // (0 off, 1 on, 2 on with register prefetch)
+extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
@@ -2756,6 +2757,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 6) {
     const int prev = g_igemm_nr;
     g_igemm_nr = value ? 1 : 0;
+    return prev;
+  }
+  if (key == 8) {  // bn.hip: buffer-resource BatchNorm bodies
+    const int prev = g_bn_v2;
+    g_bn_v2 = value ? 1 : 0;
     return prev;
   }
   if (key == 7) {

@@ -40,6 +40,7 @@ struct WGN {
   int dy_ps, cout;
   int tiles_h, tiles_w, ntiles, tps;
   int n_ci_slabs;
+  FastDiv per_img_div, tiles_w_div;  // tile index -> (image, tile row, tile column)
   uint32_t x_bytes, dy_bytes;
   float* part;  // [splits][cout][9 * cin4], column = (dh * 3 + dw) * cin4 + ci
   // x is the pre-BN output of a BatchNorm(+ReLU) layer whose normalised activation is never
@@ -63,8 +64,6 @@ __global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
   constexpr int G = (3 * CSW + 15) / 16;         // 16-column groups per dw
   constexpr int WCOL = 4 / WPIX;
   constexpr int GW = (G + WCOL - 1) / WCOL;      // groups per wave
-  constexpr int NXI = (LPX * CQ + 255) / 256;    // X quads per thread
-  constexpr int NDI = (kNPX * COQ + 255) / 256;  // dY quads per thread
   static_assert(NR <= 4 && (NR == 0 || COQ == 4 * TM + 1), "one remainder quad");
   static_assert(WPIX == 1 || WPIX == 2 || WPIX == 4, "waves per tile");
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -125,61 +124,61 @@ __global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
   const int per_img = p.tiles_h * p.tiles_w;
   const int tb = blockIdx.x * p.tps;
   const int te = tb + p.tps < p.ntiles ? tb + p.tps : p.ntiles;
+  // staging map: thread -> one channel quad (fixed) and pixels b, b + XPU, b + 2 XPU, ...
+  // (no per-item division by the quad count)
+  constexpr int XPU = 256 / CQ, DPU = 256 / COQ;  // pixels per pass
+  constexpr int NXI = (LPX + XPU - 1) / XPU, NDI = (kNPX + DPU - 1) / DPU;
+  const int xq = threadIdx.x % CQ, xb = threadIdx.x / CQ;     // xb < XPU: active
+  const int dq = threadIdx.x % COQ, db = threadIdx.x / COQ;
+  const bool xact = xb < XPU, dact = db < DPU;
+  const int xc = c0 + 4 * xq;
+  const bool xcok = xc < p.cin4;
+  const bool dcok = co0 + 4 * dq < p.cout;
   f4 px[NXI], pd[NDI];
   uint32_t xin = 0;  // in-image X items (input BatchNorm)
   auto fetch = [&](int tile) {
-    const int img = tile / per_img;
+    const int img = (int)p.per_img_div.div((uint32_t)tile);
     const int trem = tile - img * per_img;
-    const int th = trem / p.tiles_w;
+    const int th = (int)p.tiles_w_div.div((uint32_t)trem);
     const int oh0 = th * kTH, ow0 = (trem - th * p.tiles_w) * kTW;
     const int ibase = img * p.h;
 #pragma unroll
     for (int u = 0; u < NXI; ++u) {
-      int i = threadIdx.x + u * 256;
-      asm volatile("" : "+v"(i));  // recomputed per tile, not held in registers across tiles
-      const int hp = i / CQ, q = i - hp * CQ;
+      const int hp = xb + u * XPU;
       const int lr = hp / kLW, lc = hp - lr * kLW;
       const int ih = oh0 - 1 + lr, iw = ow0 - 1 + lc;
-      const bool ok = i < LPX * CQ && (unsigned)ih < (unsigned)p.h && (unsigned)iw < (unsigned)p.w &&
-                      c0 + 4 * q < p.cin4;
-      px[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + c0 + 4 * q) * 4u : kOOB);
+      const bool ok = xact && hp < LPX && xcok && (unsigned)ih < (unsigned)p.h &&
+                      (unsigned)iw < (unsigned)p.w;
+      px[u] = load4(xr, ok ? (uint32_t)(((ibase + ih) * p.w + iw) * p.x_ps + xc) * 4u : kOOB);
       xin = u == 0 ? (uint32_t)ok : (xin | ((uint32_t)ok << u));
     }
 #pragma unroll
     for (int u = 0; u < NDI; ++u) {
-      int i = threadIdx.x + u * 256;
-      asm volatile("" : "+v"(i));
-      const int pp = i / COQ, q = i - pp * COQ;
+      const int pp = db + u * DPU;
       const int oh = oh0 + pp / kTW, ow = ow0 + (pp & (kTW - 1));
-      const bool ok = i < kNPX * COQ && oh < p.h && ow < p.w && co0 + 4 * q < p.cout;
-      pd[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co0 + 4 * q) * 4u : kOOB);
+      const bool ok = dact && pp < kNPX && dcok && oh < p.h && ow < p.w;
+      pd[u] = load4(dr, ok ? (uint32_t)(((ibase + oh) * p.w + ow) * p.dy_ps + co0 + 4 * dq) * 4u : kOOB);
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int u = 0; u < NXI; ++u) {
-      int i = threadIdx.x + u * 256;
-      asm volatile("" : "+v"(i));
-      if (LPX * CQ % 256 != 0 && i >= LPX * CQ) break;
-      const int hp = i / CQ, q = i - hp * CQ;
-      const int c = c0 + 4 * q;
+      const int hp = xb + u * XPU;
+      if (!xact || hp >= LPX) break;
       f4 v = px[u];
-      if (p.isave && ((xin >> u) & 1u)) ibn(v, q);
+      if (p.isave && ((xin >> u) & 1u)) ibn(v, xq);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = c + k < p.cin ? v[k] : 0.f;  // channel padding
-      *reinterpret_cast<f4*>(&xs[hp * XP + 4 * q]) = v;
+      for (int k = 0; k < 4; ++k) v[k] = xc + k < p.cin ? v[k] : 0.f;  // channel padding
+      *reinterpret_cast<f4*>(&xs[hp * XP + 4 * xq]) = v;
     }
 #pragma unroll
     for (int u = 0; u < NDI; ++u) {
-      int i = threadIdx.x + u * 256;
-      asm volatile("" : "+v"(i));
-      if (kNPX * COQ % 256 != 0 && i >= kNPX * COQ) break;
-      const int pp = i / COQ, q = i - pp * COQ;
-      const int co = co0 + 4 * q;
+      const int pp = db + u * DPU;
+      if (!dact || pp >= kNPX) break;
       f4 v = pd[u];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = (co + k < p.cout && 4 * q + k < CO) ? v[k] : 0.f;
-      *reinterpret_cast<f4*>(&ds[pp * DP + 4 * q]) = v;
+      for (int k = 0; k < 4; ++k) v[k] = (co0 + 4 * dq + k < p.cout && 4 * dq + k < CO) ? v[k] : 0.f;
+      *reinterpret_cast<f4*>(&ds[pp * DP + 4 * dq]) = v;
     }
   };
 
@@ -242,18 +241,25 @@ __global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
         racc[j][d][q] = v;
       }
   const int ncol4 = 9 * p.cin4;
-  float* out = p.part + (int64_t)blockIdx.x * p.cout * ncol4;
-  auto write = [&](int j, int d, int i, int e, float v) {
+  // part[split][co][col]: this block's slab through a buffer resource (32-bit offsets)
+  const uint32_t slab = (uint32_t)(p.cout * ncol4);
+  const __amdgpu_buffer_rsrc_t orr = make_rsrc(p.part + (int64_t)blockIdx.x * slab, slab * 4u);
+  int colb[GW];  // column of (dh, ci) at dw = 0, or -1
+#pragma unroll
+  for (int j = 0; j < GW; ++j) {
     const int n = (wc * GW + j) * 16 + r;
     const int dh = n / CSW, ci = n - dh * CSW;
+    colb[j] = colok[j] ? dh * 3 * p.cin4 + c0 + ci : -1;
+  }
+  auto write = [&](int j, int d, int i, int e, float v) {
     const int co = co0 + 16 * i + 4 * g + e;
-    if (colok[j] && co < p.cout) out[(int64_t)co * ncol4 + (dh * 3 + d) * p.cin4 + c0 + ci] = v;
+    const bool ok = colb[j] >= 0 && co < p.cout;
+    store1(orr, ok ? (uint32_t)(co * ncol4 + colb[j] + d * p.cin4) * 4u : kOOB, v);
   };
   auto write_r = [&](int j, int d, int q, float v) {
-    const int n = (wc * GW + j) * 16 + r;
-    const int dh = n / CSW, ci = n - dh * CSW;
     const int co = co0 + 16 * TM + q;
-    if (g == 0 && colok[j] && co < p.cout) out[(int64_t)co * ncol4 + (dh * 3 + d) * p.cin4 + c0 + ci] = v;
+    const bool ok = g == 0 && colb[j] >= 0 && co < p.cout;
+    store1(orr, ok ? (uint32_t)(co * ncol4 + colb[j] + d * p.cin4) * 4u : kOOB, v);
   };
   if constexpr (WPIX == 1) {
 #pragma unroll
@@ -419,6 +425,8 @@ int wgrad3n_launch(const float* x, const vae2_act* xd, const float* dy, const va
   p.dy = dy; p.dy_ps = (int)dyd->ps; p.cout = (int)dyd->c;
   p.tiles_h = pl.tiles_h; p.tiles_w = pl.tiles_w; p.ntiles = pl.ntiles; p.tps = pl.tps;
   p.n_ci_slabs = pl.c.ci_slabs;
+  p.per_img_div = FastDiv((uint32_t)(pl.tiles_h * pl.tiles_w));
+  p.tiles_w_div = FastDiv((uint32_t)pl.tiles_w);
   p.x_bytes = x_bytes; p.dy_bytes = dy_bytes;
   p.part = part;
   p.isave = isave; p.irelu = irelu ? 1 : 0;

@@ -41,6 +41,10 @@ _SCHEMA = {
     # build-only switches (not in the reference)
     "MI355X": {
         "SYNC_BN": True,          # global BN statistics when distributed (reference: SyncBatchNorm)
+        # SyncBN statistics exchange: "ipc" = the one-shot peer all-reduce kernel
+        # (vae2_syncbn_allreduce, node-local, self-checked at start; RCCL if it does not come
+        # up), "rccl" = torch.distributed all_reduce
+        "SYNC_BN_EXCHANGE": "ipc",
         "HIP_GRAPH": False,       # capture the training step in a hipGraph
         "DEFER_CHECKS": False,    # one NaN/Inf host read per step instead of four
         "SYNTHETIC_DATA": False,  # Cityscapes-shaped Gaussian clips instead of the zip dataset

@@ -39,8 +39,13 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--relu", type=int, default=1)
     ap.add_argument("--res", type=int, default=1)
+    ap.add_argument("--tune", default="", help="vae2_conv2d_set_tune key=value[,key=value]")
+    ap.add_argument("--mask", type=int, default=0, help="ReLU mask bytes (residual layers)")
     a = ap.parse_args()
-    _lib.load()
+    lib = _lib.load()
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        lib.vae2_conv2d_set_tune(int(k), int(v))
     dev = torch.device("cuda")
     shapes = [(128, 256, 18), (64, 128, 36), (32, 64, 72), (16, 32, 144)]
     lay = (_lib.BnLayer * len(shapes))()
@@ -57,6 +62,10 @@ def main():
         keep += [x, y, r, dy, dx, dres, save, gamma, part, sums]
         lay[i] = _bn_layer(x, r if a.res else None, y, dy, dres if a.res else None, save, gamma,
                            part, sums.data_ptr(), None, float(a.n * h * w), a.relu)
+        if a.mask:  # ReLU mask bytes instead of y in the backward passes (residual layers)
+            mk = torch.randint(0, 16, (a.n * h * w * ((c + 3) // 4),), dtype=torch.uint8, device=dev)
+            keep.append(mk)
+            lay[i].mask = mk.data_ptr()
         t = 4 * a.n * h * w * c
         nbytes["apply"] += t * (3 if a.res else 2)
         nbytes["bwd_reduce"] += t * (3 if a.res else 2)

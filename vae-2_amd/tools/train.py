@@ -138,6 +138,8 @@ def main(argv=None):
     if distributed:
         vdist.init("nccl")
         vdist.set_sync_bn(config.MI355X.SYNC_BN)
+        if config.MI355X.SYNC_BN and config.MI355X.SYNC_BN_EXCHANGE == "ipc":
+            vdist.init_syncbn_ipc()
     device = torch.device("cuda:{}".format(args.local_rank))
     torch.cuda.set_device(device)
 

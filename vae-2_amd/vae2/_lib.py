@@ -156,6 +156,12 @@ _SIGS = {
     "vae2_adam_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                                c_i64, c_vp]),
     "vae2_scale": (c_int, [c_vp, c_vp, c_i64, c_f32, c_vp]),
+    "vae2_syncbn_comm_bytes": (c_i64, [c_int, c_i64]),
+    "vae2_syncbn_comm_init": (c_int, [c_int, c_int, c_i64, c_vp, ctypes.POINTER(c_vp)]),
+    "vae2_syncbn_comm_connect": (c_int, [c_vp, c_vp]),
+    "vae2_syncbn_allreduce": (c_int, [c_vp, c_vp, c_i64, c_vp]),
+    "vae2_syncbn_comm_error": (c_int, [c_vp, ctypes.POINTER(c_i64)]),
+    "vae2_syncbn_comm_destroy": (c_int, [c_vp]),
     "vae2_clip_normalize_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int,
                                        ctypes.POINTER(c_vp), c_vp]),
     "vae2_to_image": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
@@ -174,7 +180,7 @@ _SIGS = {
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _lib = None
 
 

@@ -86,6 +86,99 @@ def all_reduce_(t, group=None):
         dist.all_reduce(t, group=group)
 
 
+# ---- SyncBN statistics: one-shot IPC peer all-reduce (vae2_syncbn_allreduce) ----
+_SB = None  # (comm, group, max_elems)
+SB_MAX_ELEMS = 1 << 15  # doubles per exchange (a depth level's sums: <= 6 x 2 x 512 + 6)
+
+
+def init_syncbn_ipc(group=None, max_elems=SB_MAX_ELEMS):
+    """Route the SyncBN statistics exchanges of `group` (default: the SyncBN group) through
+    the one-shot peer all-reduce kernel (csrc/syncbn.hip) instead of RCCL: one kernel per
+    exchange, every rank's payload stored into every rank's IPC-mapped receive area over
+    xGMI, summed in rank order.  Collective over the group; node-local ranks only
+    (LOCAL_WORLD_SIZE == world).  A self-check exchange of rank-dependent values must give
+    the exact sums on every rank, else RCCL stays in use.  Returns True when active."""
+    global _SB
+    import ctypes
+    from ._lib import load
+    if not is_dist():
+        return False
+    g = group if group is not None else (sync_bn_group() or dist.group.WORLD)
+    if dist.get_backend(g) == "gloo" and not FORCE_IPC:
+        return False
+    world, rk = dist.get_world_size(g), dist.get_rank(g)
+    if world > 8 or int(os.environ.get("LOCAL_WORLD_SIZE", world)) != dist.get_world_size():
+        return False  # (several nodes: IPC maps only the node's own GPUs)
+    lib = load()
+    comm = ctypes.c_void_p()
+    h = ctypes.create_string_buffer(64)
+    ok = lib.vae2_syncbn_comm_init(rk, world, max_elems, h, ctypes.byref(comm)) == 0
+    hs = [None] * world
+    dist.all_gather_object(hs, h.raw if ok else None, group=g)
+    if all(x is not None for x in hs):
+        ok = ok and lib.vae2_syncbn_comm_connect(comm, b"".join(hs)) == 0
+    else:
+        ok = False
+    if ok:  # self-check: exact small-integer sums, every rank
+        t = torch.arange(1, 65, dtype=torch.float64, device=torch.cuda.current_device()) * (rk + 1)
+        ok = lib.vae2_syncbn_allreduce(comm, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+        torch.cuda.synchronize()
+        err = ctypes.c_int64(0)
+        lib.vae2_syncbn_comm_error(comm, ctypes.byref(err))
+        want = torch.arange(1, 65, dtype=torch.float64) * (world * (world + 1) / 2)
+        ok = ok and err.value == 0 and torch.equal(t.cpu(), want)
+    flags = [None] * world
+    dist.all_gather_object(flags, bool(ok), group=g)
+    if not all(flags):
+        if comm.value:
+            lib.vae2_syncbn_comm_destroy(comm)
+        return False
+    # every exchange runs on this one stream, in host issue order (the same order on every
+    # rank): the kernel's sequence numbers pair each exchange with the peers' same exchange
+    # even when the step issues them from several streams (posterior net, past decoder)
+    _SB = (comm, g, max_elems, torch.cuda.Stream())
+    return True
+
+
+FORCE_IPC = False  # tests: the IPC exchange under a gloo group (ranks sharing one GPU)
+
+
+def syncbn_exchange():
+    """'ipc' when the one-shot peer all-reduce carries the SyncBN statistics, else 'rccl' /
+    the group's backend."""
+    return "ipc" if _SB is not None else (dist.get_backend(sync_bn_group())
+                                          if sync_bn_group() is not None else "none")
+
+
+def syncbn_all_reduce_(t, group=None):
+    """In-place sum of a SyncBN statistics buffer over the SyncBN group (float64)."""
+    if _SB is not None and t.is_cuda and t.dtype == torch.float64 and t.numel() <= _SB[2] and \
+            (group is None or group is _SB[1] or group == _SB[1]) and t.is_contiguous():
+        import ctypes
+        from ._lib import call
+        cur, cs = torch.cuda.current_stream(), _SB[3]
+        cs.wait_stream(cur)
+        call("vae2_syncbn_allreduce", _SB[0], ctypes.c_void_p(t.data_ptr()), t.numel(),
+             ctypes.c_void_p(cs.cuda_stream))
+        cur.wait_stream(cs)
+        return
+    all_reduce_(t, group=group)
+
+
+def syncbn_check():
+    """Raise if a SyncBN exchange timed out (a peer missing: the kernel gave up after 60 s
+    instead of hanging).  Synchronous; call at a logging point, not per step."""
+    if _SB is None:
+        return
+    import ctypes
+    from ._lib import load
+    err = ctypes.c_int64(0)
+    load().vae2_syncbn_comm_error(_SB[0], ctypes.byref(err))
+    if err.value:
+        raise RuntimeError("SyncBN IPC exchange timed out (a rank did not arrive)")
+
+
 def bucket_allreduce(buf, bucket_elems=BUCKET_ELEMS, group=None):
     """Sum-all-reduce a flat buffer in fixed-size buckets (same bucket boundaries on
     every rank, issued in order)."""

@@ -110,7 +110,7 @@ def _all_reduce_sums(sums, count, group):
     if group is None:
         return sums, count
     from . import dist as vdist
-    vdist.all_reduce_(sums, group=group)  # in place: the callers' sums are fresh buffers
+    vdist.syncbn_all_reduce_(sums, group=group)  # in place: the callers' sums are fresh buffers
     return sums, count * dist.get_world_size(group)
 
 
@@ -782,7 +782,7 @@ class _ConvBNMulti(torch.autograd.Function):
         else:  # SyncBN: one exchange of every layer's (sum x, sum x^2) and count
             call("vae2_bn_multi_reduce", n, arr, 2, s)
             from . import dist as vdist
-            vdist.all_reduce_(buf, group=group)
+            vdist.syncbn_all_reduce_(buf, group=group)
             call("vae2_bn_multi_finalize", n, arr, s)
         ys, lay = [], []
         masks = [None] * n
@@ -935,7 +935,7 @@ class _ConvBNMulti(torch.autograd.Function):
         call("vae2_bn_multi_reduce", n, fins, 1, s)  # local sums + dgamma / dbeta
         if group is not None:  # SyncBN: global (sum g, sum g*xhat) for the input gradients
             from . import dist as vdist
-            vdist.all_reduce_(buf, group=group)
+            vdist.syncbn_all_reduce_(buf, group=group)
         if prof.active():
             prof.note(0, sum(4.0 * rs[i].numel() * (3 + _y_reads(ctx, i) +
                                                     (1 if dress[i][0] is not None else 0) +
