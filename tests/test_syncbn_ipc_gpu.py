@@ -86,6 +86,15 @@ def _work(rank, world, port, q):
         for k, b in enumerate(bufs):
             want = sum(float(r + 1) * (it + 1) + k for r in range(world))
             gok &= bool((b.cpu() == want).all())
+    # latency inside a replayed graph (how the training step issues them): 6 exchanges of
+    # 512 doubles + 6 copies per replay
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        g.replay()
+    torch.cuda.synchronize()
+    us_graph = (time.perf_counter() - t0) / (200 * 6) * 1e6
     # latency: back-to-back exchanges of a depth level's statistics (2048 doubles)
     t = torch.randn(2048, dtype=torch.float64, device="cuda")
     dist.barrier()
@@ -96,7 +105,7 @@ def _work(rank, world, port, q):
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / 500 * 1e6
     vdist.syncbn_check()
-    q.put((rank, "ok", ok, gok, us))
+    q.put((rank, "ok", ok, gok, us, us_graph))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -132,7 +141,8 @@ def test_syncbn_ipc_two_ranks_exact_sums():
         p.join(timeout=60)
     errors = [r for r in res if r[1] == "error"]
     assert not errors, errors[0][2]
-    for rank, _, ok, gok, us in sorted(res):
-        print(f"rank {rank}: exact {ok}, graph replay {gok}, {us:.1f} us per 2048-double exchange")
+    for rank, _, ok, gok, us, usg in sorted(res):
+        print(f"rank {rank}: exact {ok}, graph replay {gok}, {us:.1f} us per 2048-double exchange "
+              f"(eager issue), {usg:.1f} us per exchange in a replayed graph")
         assert ok, "eager exchanges differ from the rank-order sums"
         assert gok, "graph-replayed exchanges wrong"

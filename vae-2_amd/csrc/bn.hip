@@ -1042,6 +1042,12 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnLayer& L, int blk) {
 // 308 SALU instructions per wave (64-bit addresses, per-channel scalar coefficient loads,
 // exec-mask branches around the partial-quad stores), 40 % of wave cycles in issue stalls.
 // Every tensor extent < 2 GB (host check, bn_multi_launch).
+// ACT (compile time, so the unused operand arrays cost no registers): how the ReLU mask is
+// known -- 0 recomputed from x (or no ReLU), 1 mask bytes, 2 stored y, 3 decided per layer;
+// RB: some layer has a residual BatchNorm (rx); DACC: some layer accumulates onto dres.
+// (The all-features body held 158 VGPRs: 3 workgroups per CU, a narrow 3-layer launch of
+// ~2,200 workgroups ran in ~3 rounds.)
+template <int ACT, bool RB, bool DACC>
 __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
   const int C = L.C, c4 = (C + 3) >> 2;
   const int tid = threadIdx.x;
@@ -1051,9 +1057,9 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
   const bool part = (C & 3) != 0;        // (uniform) some quad is partial
   const uint32_t P = (uint32_t)L.P;
   const bool relu = L.relu != 0;
-  const bool usemk = relu && L.mk != nullptr;
-  const bool usey = relu && !usemk && L.a != nullptr;
-  const bool rb = L.rx != nullptr;
+  const bool usemk = relu && (ACT == 1 || (ACT == 3 && L.mk != nullptr));
+  const bool usey = relu && (ACT == 2 || (ACT == 3 && L.mk == nullptr && L.a != nullptr));
+  const bool rb = RB && L.rx != nullptr;
   const bool dres = L.dres != nullptr;
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(L.dy, P * (uint32_t)L.dy_ps * 4u);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(L.x, P * (uint32_t)L.x_ps * 4u);
@@ -1074,12 +1080,12 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
     gv[u] = load4(rdy, (pp[u] * (uint32_t)L.dy_ps + (uint32_t)c) * 4u);
     xv[u] = load4(rx, (pp[u] * (uint32_t)L.x_ps + (uint32_t)c) * 4u);
   }
-  if (usey) {
+  if ((ACT == 2 || ACT == 3) && usey) {
     const __amdgpu_buffer_rsrc_t ry = make_rsrc(L.a, P * (uint32_t)L.a_ps * 4u);
 #pragma unroll
     for (int u = 0; u < kApplyU; ++u) yv[u] = load4(ry, (pp[u] * (uint32_t)L.a_ps + (uint32_t)c) * 4u);
   }
-  if (usemk) {
+  if ((ACT == 1 || ACT == 3) && usemk) {
     const __amdgpu_buffer_rsrc_t rm = make_rsrc(L.mk, P * (uint32_t)c4);
 #pragma unroll
     for (int u = 0; u < kApplyU; ++u) mv[u] = load_u8(rm, pp[u] * (uint32_t)c4 + (uint32_t)(c >> 2));
@@ -1090,7 +1096,8 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
     for (int u = 0; u < kApplyU; ++u) rxv[u] = load4(rr, (pp[u] * (uint32_t)L.rx_ps + (uint32_t)c) * 4u);
   }
   const __amdgpu_buffer_rsrc_t rdr = make_rsrc(L.dres, dres ? P * (uint32_t)L.dres_ps * 4u : 0u);
-  if (dres && L.dres_acc) {
+  const bool dacc = DACC && dres && L.dres_acc;
+  if (dacc) {
 #pragma unroll
     for (int u = 0; u < kApplyU; ++u) dv[u] = load4(rdr, (pp[u] * (uint32_t)L.dres_ps + (uint32_t)c) * 4u);
   }
@@ -1147,8 +1154,8 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       bool pos;
-      if (usemk) pos = ((mv[u] >> k) & 1u) != 0;
-      else if (usey) pos = yv[u][k] > 0.f;
+      if ((ACT == 1 || ACT == 3) && usemk) pos = ((mv[u] >> k) & 1u) != 0;
+      else if ((ACT == 2 || ACT == 3) && usey) pos = yv[u][k] > 0.f;
       else pos = __builtin_fmaf(xv[u][k], sc[k], sh[k]) > 0.f;
       if (relu && !pos) g[k] = 0.f;
       const float xh = (xv[u][k] - mean[k]) * invstd[k];
@@ -1157,7 +1164,7 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
     const uint32_t po = in[u] ? pp[u] : 0x7fffffffu;  // pixels past P: dropped stores
     auto off = [&](int ps) { return in[u] ? (po * (uint32_t)ps + (uint32_t)c) * 4u : kOOB; };
     if (dres) {
-      const f4 dr = L.dres_acc ? g + dv[u] : g;
+      const f4 dr = dacc ? g + dv[u] : g;
       if (part) store_quad(rdr, off(L.dres_ps), dr, nv);
       else store4(rdr, off(L.dres_ps), dr);
     }
@@ -1176,9 +1183,37 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
   }
 }
 
+template <int ACT, bool RB, bool DACC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
   const int i = bn_layer_of(m, blockIdx.x);
-  bn_bwd_apply_body2(m.L[i], blockIdx.x - m.L[i].blk0);
+  bn_bwd_apply_body2<ACT, RB, DACC>(m.L[i], blockIdx.x - m.L[i].blk0);
+}
+
+// The specialisation of a launch: the union of its layers' features.
+static void bwd_apply_launch(const BnMulti& m, unsigned blocks, hipStream_t st) {
+  int act = -1;
+  bool rb = false, dacc = false;
+  for (int j = 0; j < m.n; ++j) {
+    const BnLayer& L = m.L[j];
+    const int a = !L.relu ? 0 : (L.mk ? 1 : (L.a ? 2 : 0));
+    act = act < 0 ? a : (act == a ? act : 3);
+    rb = rb || L.rx;
+    dacc = dacc || (L.dres && L.dres_acc);
+  }
+#define BWA(A)                                                                                  \
+  do {                                                                                          \
+    if (rb && dacc) VAE2_LAUNCH((bn_bwd_apply_multi_kernel<A, true, true>), dim3(blocks), dim3(256), 0, st, m); \
+    else if (rb) VAE2_LAUNCH((bn_bwd_apply_multi_kernel<A, true, false>), dim3(blocks), dim3(256), 0, st, m);   \
+    else if (dacc) VAE2_LAUNCH((bn_bwd_apply_multi_kernel<A, false, true>), dim3(blocks), dim3(256), 0, st, m); \
+    else VAE2_LAUNCH((bn_bwd_apply_multi_kernel<A, false, false>), dim3(blocks), dim3(256), 0, st, m);          \
+  } while (0)
+  switch (act) {
+    case 0: BWA(0); break;
+    case 1: BWA(1); break;
+    case 2: BWA(2); break;
+    default: BWA(3); break;
+  }
+#undef BWA
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_r4_kernel(BnMulti m) {
@@ -1592,7 +1627,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
     else if (kind == 1)
       VAE2_LAUNCH(bn_bwd_reduce_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     else if (m.v2)
-      VAE2_LAUNCH(bn_bwd_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+      bwd_apply_launch(m, (unsigned)blocks, st);
     else
       VAE2_LAUNCH(bn_bwd_apply_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     const int rc = check_launch(fn);

@@ -1039,8 +1039,13 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
             if j is None:
                 continue
             if (residuals[i] is not None or residuals[j] is not None or relus[j] or
-                    res_bns[j] is not None or (bn_outs is not None and bn_outs[i] is not None)):
+                    res_bns[j] is not None or (bn_outs is not None and
+                                               (bn_outs[i] is not None or bn_outs[j] is not None))):
                 raise ValueError("res_bns: the shortcut layer must be a plain conv + BN")
+            shp = [(xs[k].shape[0], *specs[k].out_hw(xs[k].shape[1], xs[k].shape[2]),
+                    convs[k].out_channels) for k in (i, j)]
+            if shp[0] != shp[1]:
+                raise ValueError(f"res_bns: shortcut output {shp[1]} != layer output {shp[0]}")
             specs[i].res_bn = j
             specs[j].bn_out = ResBN()
     if (not BN_BATCH or not RES_BN and res_bns is not None and any(j is not None for j in res_bns)
