@@ -830,7 +830,9 @@ __device__ __forceinline__ void bn_bwd_reduce_body(const BnLayer& L, int blk, in
   }
 }
 
-// Buffer-resource form of bn_bwd_reduce_body (same arithmetic and summation order).
+// Buffer-resource form of bn_bwd_reduce_body (same arithmetic and summation order),
+// specialised like bn_bwd_apply_body2 (ACT: ReLU mask source, RB: residual BatchNorm).
+template <int ACT, bool RB>
 __device__ __forceinline__ void bn_bwd_reduce_body2(const BnLayer& L, int blk, int nblk,
                                                    float* red0, float* red1) {
   const int C = L.C, c4 = (C + 3) >> 2;
@@ -840,9 +842,10 @@ __device__ __forceinline__ void bn_bwd_reduce_body2(const BnLayer& L, int blk, i
   if (p1 > L.P) p1 = L.P;
   f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s0;
   const int r = tid / c4, c = 4 * (tid - r * c4);
-  const uint8_t* mk = L.relu ? L.mk : nullptr;  // stored mask, else y, else from x
-  const float* y = L.relu && !mk ? L.a : nullptr;
-  const bool rb = L.rx != nullptr;  // + the residual BN's sum g * xhat_r (same g)
+  // stored mask, else y, else from x (ACT 0 / 1 / 2 fixed at compile time, 3 per layer)
+  const uint8_t* mk = L.relu && (ACT == 1 || ACT == 3) ? L.mk : nullptr;
+  const float* y = L.relu && (ACT == 2 || (ACT == 3 && !mk)) ? L.a : nullptr;
+  const bool rb = RB && L.rx != nullptr;  // + the residual BN's sum g * xhat_r (same g)
   const uint32_t P = (uint32_t)L.P;
   const __amdgpu_buffer_rsrc_t rxx = make_rsrc(L.x, P * (uint32_t)L.x_ps * 4u);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(L.dy, P * (uint32_t)L.dy_ps * 4u);
@@ -930,11 +933,35 @@ __device__ __forceinline__ void bn_bwd_reduce_body2(const BnLayer& L, int blk, i
 }
 
 // nblk of layer i = blk0[i+1] - blk0[i] (the last: gridDim.x - blk0)
+template <int ACT, bool RB>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_multi_kernel(BnMulti m) {
   __shared__ float red[2][256 * 4];
   const int i = bn_layer_of(m, blockIdx.x);
   const int nblk = (i + 1 < m.n ? m.L[i + 1].blk0 : (int)gridDim.x) - m.L[i].blk0;
-  bn_bwd_reduce_body2(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
+  bn_bwd_reduce_body2<ACT, RB>(m.L[i], blockIdx.x - m.L[i].blk0, nblk, red[0], red[1]);
+}
+
+static void bwd_reduce_launch(const BnMulti& m, unsigned blocks, hipStream_t st) {
+  int act = -1;
+  bool rb = false;
+  for (int j = 0; j < m.n; ++j) {
+    const BnLayer& L = m.L[j];
+    const int a = !L.relu ? 0 : (L.mk ? 1 : (L.a ? 2 : 0));
+    act = act < 0 ? a : (act == a ? act : 3);
+    rb = rb || L.rx;
+  }
+#define BWR(A)                                                                                    \
+  do {                                                                                            \
+    if (rb) VAE2_LAUNCH((bn_bwd_reduce_multi_kernel<A, true>), dim3(blocks), dim3(256), 0, st, m); \
+    else VAE2_LAUNCH((bn_bwd_reduce_multi_kernel<A, false>), dim3(blocks), dim3(256), 0, st, m);   \
+  } while (0)
+  switch (act) {
+    case 0: BWR(0); break;
+    case 1: BWR(1); break;
+    case 2: BWR(2); break;
+    default: BWR(3); break;
+  }
+#undef BWR
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_reduce_multi_r4_kernel(BnMulti m) {
@@ -1623,7 +1650,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
     else if (kind == 0)
       VAE2_LAUNCH(bn_apply_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     else if (kind == 1 && m.v2)
-      VAE2_LAUNCH(bn_bwd_reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
+      bwd_reduce_launch(m, (unsigned)blocks, st);
     else if (kind == 1)
       VAE2_LAUNCH(bn_bwd_reduce_multi_r4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     else if (m.v2)
