@@ -6,6 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-sq}
 ONLY=${2:-3}
 REGEX=${3:-dconv3_kernel}
+EXTRA=${4:-}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1
@@ -20,7 +21,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   echo "pass $i:$ok"
   timeout -s KILL 120 rocprofv3 --pmc $ok --kernel-include-regex "$REGEX" -f csv \
     -d gpurun_out/${TAG}_p$i -o run -- python vae-2_amd/tools/conv_bench.py --only $ONLY \
-    --iters 5 > gpurun_out/${TAG}_p$i.log 2>&1
+    --iters 5 $EXTRA > gpurun_out/${TAG}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -ne 0 ] && { tail -5 gpurun_out/${TAG}_p$i.log; exit $rc; }
 done

@@ -109,7 +109,7 @@ def test_direct_conv3x3(shape):
         torch.cuda.synchronize()
         if k == 3:
             name = ctypes_name(xg, (n, h, w, cout))
-            assert name.startswith("dconv3_kernel"), name
+            assert name.startswith(("dconv3_kernel", "dconv3s_kernel")), name
     finally:
         lib.vae2_conv2d_set_algo(prev)
     assert rel(nchw(yg), y_ref) < TOL
@@ -172,10 +172,11 @@ def test_direct_conv3x3_valu_remainder(shape):
     for c in (cout, cin):
         nr = c % 16
         if nr in (2, 4, 8) and c // 16 in (1, 2, 4):
-            # dconv3_kernel<TM, TN, FLIP, BF, NR, BNX>
-            assert any(k.startswith("dconv3_kernel") and
-                       k[:-1].split(", ")[4:5] == [str(nr)] for k in names), \
-                (c, names)
+            # dconv3_kernel<TM, TN, FLIP, BF, NR, BNX> or (18 -> 18, 36 -> 36: the
+            # streaming kernel) dconv3s_kernel<TN, NR, Q, FLIP, BNX>
+            assert any((k.startswith("dconv3_kernel") and k[:-1].split(", ")[4:5] == [str(nr)]) or
+                       (k.startswith("dconv3s_kernel") and k[:-1].split(", ")[1:2] == [str(nr)])
+                       for k in names), (c, names)
     assert rel(nchw(yg), y_ref) < TOL
     assert rel(nchw(xg.grad), x.grad) < TOL
     assert rel(cg.weight.grad, conv.weight.grad) < TOL

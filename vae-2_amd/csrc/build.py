@@ -18,14 +18,14 @@ DEFS = os.environ.get("VAE2_DEFS", "").split()
 OUT = os.path.join(PKG, f"libvae2_hip_{TAG}.so" if TAG else "libvae2_hip.so")
 BUILD = os.path.join(HERE, f"build_{TAG}" if TAG else "build")
 SOURCES = ["conv.hip", "bn.hip", "resample.hip", "elbo.hip", "heads.hip", "clips.hip",
-           "metrics.hip", "wgrad_narrow.hip", "syncbn.hip"]
+           "metrics.hip", "wgrad_narrow.hip", "syncbn.hip", "dconv_stream.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "vae2_hip.h")]
 ARCH = os.environ.get("VAE2_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
          "-Wno-unused-function", "-munsafe-fp-atomics"]
 # per-source extras: no SLP vectorisation in the conv kernels (it packs independent f32
 # FMAs beside the MFMAs into v_pk_fma_f32 + operand moves, which cost issue slots there)
-EXTRA = {"conv.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"conv.hip": ["-fno-slp-vectorize"], "dconv_stream.hip": ["-fno-slp-vectorize"]}
 # conv.hip is compiled as four objects (VAE2_CONV_PART 0..3: pack + C-ABI dispatch, gather
 # kernels, direct 3x3 kernels, weight-gradient kernels) so its instantiations build in
 # parallel

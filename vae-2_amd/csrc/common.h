@@ -100,6 +100,35 @@ __device__ __forceinline__ void store_quad(__amdgpu_buffer_rsrc_t r, uint32_t of
   store1(r, (n & 1) ? off + 4u * (uint32_t)(n & 2) : kOOB, (n & 2) ? v[2] : v[0]);
 }
 
+// Bijective blockIdx remap (T1): blocks are dealt round-robin over the 8 XCDs, so
+// logical tiles are re-numbered to make each XCD own a contiguous run of tiles
+// (vertically adjacent image rows share that XCD's L2).  Speed only.
+__device__ __forceinline__ int xcd_remap(int orig, int n) {
+  const int q = n >> 3, rr = n & 7, x = orig & 7;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (orig >> 3);
+}
+
+// 4 x 4 transpose across the 4 lanes of a lane quad (DPP quad_perm, no LDS): lane k's
+// v[e] becomes lane e's former v[k].  A 16x16 MFMA accumulator (lane (g, r) = column r,
+// rows 4g..4g+3) then has lane (g, 4Q + k) holding row 4g + k, columns 4Q..4Q+3.
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
+                                                            0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
+                                                            0x4E, 0xF, 0xF, true));
+}
+__device__ __forceinline__ void quad_transpose(f4& v, int k) {
+  const bool o = k & 1;
+  float a = dpp_xor1(o ? v[0] : v[1]), b = dpp_xor1(o ? v[2] : v[3]);
+  if (o) { v[0] = a; v[2] = b; } else { v[1] = a; v[3] = b; }
+  const bool h = k & 2;
+  a = dpp_xor2(h ? v[0] : v[2]);
+  b = dpp_xor2(h ? v[1] : v[3]);
+  if (h) { v[0] = a; v[1] = b; } else { v[2] = a; v[3] = b; }
+}
+
 // ------------------------------------------------------- activations ----
 // Device-side copy of vae2_act with 32-bit-safe strides kept in 64-bit.
 struct Act {
@@ -198,6 +227,18 @@ int64_t wgrad3n_splits(const vae2_act* xd, const vae2_act* dyd);
 int wgrad3n_launch(const float* x, const vae2_act* xd, const float* dy, const vae2_act* dyd,
                    float* part, const float* isave, int irelu, uint32_t x_bytes,
                    uint32_t dy_bytes, hipStream_t s);
+
+// Internal (dconv_stream.hip): the streaming direct 3x3 kernel of the 18 / 36-channel
+// branches.  _shape: it takes this (input, output) pair; _rows: its BatchNorm partial rows
+// (workgroups); _launch: 1 when launched, 0 when the shape is not its own.
+extern int g_dconv_stream, g_dconv_stream_wpc, g_dconv_stream_bl;
+bool dconv3s_shape(const vae2_act* ad, const vae2_act* yd);
+int64_t dconv3s_rows(const vae2_act* ad, const vae2_act* yd);
+int dconv3s_launch(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
+                   const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
+                   bool flip, const float* isave, int irelu, const float* bx, int bx_ps,
+                   int brelu, const float* bsave, uint32_t bx_bytes, uint32_t a_bytes,
+                   hipStream_t s);
 
 // Internal (not part of the public ABI): dbias (+)= column sums from BN-style partials.
 int bias_grad_from_partials(const float* partials, int64_t rows, int64_t c,

@@ -48,15 +48,6 @@ namespace vae2 {
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
-// Bijective blockIdx remap (T1): blocks are dealt round-robin over the 8 XCDs, so
-// logical tiles are re-numbered to make each XCD own a contiguous run of tiles
-// (vertically adjacent image rows share that XCD's L2).  Speed only.
-__device__ __forceinline__ int xcd_remap(int orig, int n) {
-  const int q = n >> 3, rr = n & 7, x = orig & 7;
-  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (orig >> 3);
-}
-
-
 #if VAE2_PART(0)
 // ------------------------------------------------------------ weight pack ----
 // mode 0: out[n][t][c4] = w[n][c][t]         n < round_up(cout,64), c4 < round_up(cin,4)
@@ -109,28 +100,6 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const vae2_pa
 }
 
 #endif  // VAE2_PART(0)
-// 4 x 4 transpose across the 4 lanes of a lane quad (DPP quad_perm, no LDS): lane k's
-// v[e] becomes lane e's former v[k].  A 16x16 MFMA accumulator (lane (g, r) = column r,
-// rows 4g..4g+3) then has lane (g, 4Q + k) holding row 4g + k, columns 4Q..4Q+3.
-__device__ __forceinline__ float dpp_xor1(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
-                                                            0xB1, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float dpp_xor2(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
-                                                            0x4E, 0xF, 0xF, true));
-}
-__device__ __forceinline__ void quad_transpose(f4& v, int k) {
-  const bool o = k & 1;
-  float a = dpp_xor1(o ? v[0] : v[1]), b = dpp_xor1(o ? v[2] : v[3]);
-  if (o) { v[0] = a; v[2] = b; } else { v[1] = a; v[3] = b; }
-  const bool h = k & 2;
-  a = dpp_xor2(h ? v[0] : v[2]);
-  b = dpp_xor2(h ? v[1] : v[3]);
-  if (h) { v[0] = a; v[1] = b; } else { v[2] = a; v[3] = b; }
-}
-
-
 // ------------------------------------------------------------ igemm ----
 struct IGemm {
   const float* a;  // gathered activation (NHWC)
@@ -2356,10 +2325,18 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   return d;
 }
 
+// The streaming kernel (dconv_stream.hip) takes the 18 -> 18 and 36 -> 36 direct convs
+// (fp32 operands, the VALU-remainder form) wherever the direct kernel is legal: its
+// partial-statistics rows are its workgroups, so dconv_rows asks the same predicate.
+static bool stream_use(const vae2_act* ad, const vae2_act* yd) {
+  return g_dconv_stream && !g_bf16 && g_dconv_nr && g_conv_algo != 1 &&
+         (g_conv_algo == 2 || ad->w >= 16) && dconv3s_shape(ad, yd);
+}
+
 static bool dconv_use(const vae2_act* ad, const vae2_act* yd, int k, int stride, int pad,
                       const float* a) {
   if (g_conv_algo == 1 || !dconv_legal(ad, yd, k, stride, pad, a)) return false;
-  if (g_conv_algo == 2) return true;
+  if (g_conv_algo == 2 || stream_use(ad, yd)) return true;
   // auto: enough workgroups to fill the chip (narrow images waste partial 32-column
   // tiles and low-resolution layers have too few tiles: the gather kernel wins there)
   DTile d = pick_dtile(ad, yd, false);
@@ -2458,6 +2435,11 @@ static void dconv_group_launch_tn(const DConvGroup& g, int tn, dim3 grid, size_t
 int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta,
                  float* stats, bool flip, hipStream_t s, const char* fn, const BnSide& bn) {
+  if (stream_use(ad, yd)) {
+    dconv3s_launch(a, ad, wp, w_bytes, bias, y, yd, beta, stats, flip, bn.isave, bn.irelu,
+                   bn.bx, bn.bx_ps, bn.brelu, bn.bsave, bn.bx_bytes, act_bytes(ad), s);
+    return check_launch(fn);
+  }
   DTile d = pick_dtile(ad, yd);
   DConv p{};
   p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
@@ -2488,6 +2470,7 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
 #endif  // VAE2_PART(2)
 
 static int64_t dconv_rows(const vae2_act* ad, const vae2_act* yd) {
+  if (stream_use(ad, yd)) return dconv3s_rows(ad, yd);
   DTile d = pick_dtile(ad, yd);
   return ad->n * d.tiles_h * d.tiles_w;
 }
@@ -2769,6 +2752,21 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_wgrad_narrow = value >= 0 && value <= 2 ? value : 1;
     return prev;
   }
+  if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels
+    const int prev = g_dconv_stream;
+    g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
+    return prev;
+  }
+  if (key == 11) {  // dconv_stream.hip: 18-channel weights in LDS (B operand) or global
+    const int prev = g_dconv_stream_bl;
+    g_dconv_stream_bl = value ? 1 : 0;
+    return prev;
+  }
+  if (key == 10) {  // dconv_stream.hip: target workgroups per CU (0 = auto)
+    const int prev = g_dconv_stream_wpc;
+    g_dconv_stream_wpc = value >= 0 && value <= 8 ? value : 0;
+    return prev;
+  }
   return -1;
 }
 
@@ -2872,6 +2870,12 @@ int vae2_conv2d_fwd_kernel_name(const vae2_act* xd, const vae2_act* yd, int k, i
                                 int pad, char* buf, int64_t len) {
   if (!xd || !yd || !buf || len <= 0) return -22;
   if (dconv_use(xd, yd, k, stride, pad, (const float*)16)) {
+    if (stream_use(xd, yd)) {
+      const int q = (int)((xd->c + 3) / 4);
+      snprintf(buf, (size_t)len, "dconv3s_kernel<%d, %d, %d, false", q == 5 ? 1 : 2,
+               q == 5 ? 2 : 4, q);
+      return 0;
+    }
     DTile d = pick_dtile(xd, yd);
     if (d.nr)
       snprintf(buf, (size_t)len, "dconv3_kernel<%d, %d, false, false, %d>", d.tm, d.tn, d.nr);
@@ -3110,6 +3114,7 @@ int vae2_conv2d_multi(int n, const vae2_conv_job* jobs, void* stream) {
                   (fwd ? conv_shapes_ok(ad, od, J.k, J.stride, J.pad)
                        : conv_shapes_ok(od, ad, J.k, J.stride, J.pad)) &&
                   fits32(ad) && fits32(od) && dconv_use(ad, od, J.k, J.stride, J.pad, J.x) &&
+                  !stream_use(ad, od) &&         // (streaming layers: their own launch)
                   pick_dtile(ad, od).nr == 0 &&  // (remainder layers: their own launch)
                   pick_dtile(ad, od).nw == 4;    // (8-wave tiles: their own launch)
     if (!direct) {
