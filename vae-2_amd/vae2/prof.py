@@ -26,8 +26,10 @@ _ACTIVE = None
 
 # (family, regex on a kernel name), first match wins (also used by tools/trace_steps.py)
 FAMILIES = (
-    ("conv_fwd", r"dconv3_(group_)?kernel<\d+, \d+, false|igemm_kernel<\d+, \d+, \w+, 0"),
-    ("conv_dgrad", r"dconv3_(group_)?kernel<\d+, \d+, true|igemm_kernel<\d+, \d+, \w+, [12]"),
+    ("conv_fwd", r"dconv3_(group_)?kernel<\d+, \d+, false|dconv3s_kernel<\d+, \d+, \d+, false|"
+                 r"igemm_kernel<\d+, \d+, \w+, 0"),
+    ("conv_dgrad", r"dconv3_(group_)?kernel<\d+, \d+, true|dconv3s_kernel<\d+, \d+, \d+, true|"
+                   r"igemm_kernel<\d+, \d+, \w+, [12]"),
     ("conv_wgrad", r"wgrad"),
     ("conv_1x1", r"gemm1x1"),  # persistent 1x1 GEMM: forward and data gradient
     ("batchnorm", r"bn_|reduce_then|chan_partials|partials_reduce"),
