@@ -518,8 +518,14 @@ def test_stage4_module_at_bench_geometry(bench_step):
     for (n, b), (_, b64_) in zip(mg.named_buffers(), m64.named_buffers()):
         if "running" in n:
             assert max_rel(b, b64_) < 1e-5, (n, max_rel(b, b64_))
-    # every BatchNorm / fuse kernel instance of the step ran here
-    missing = sorted(_kernels(bench_step, BN_FUSE_ABI) - _kernels(rec.calls, BN_FUSE_ABI))
+    # every BatchNorm / fuse kernel instance of the step ran here, except the backward
+    # instances specialised for a residual BatchNorm (ResBN, template argument RB = true:
+    # the layer-1 Bottleneck's downsample shortcut, not part of a stage-4 module; they run
+    # in tests/test_lazy_bn_gpu.py::test_resbn_shortcut_equals_stored)
+    import re
+    resbn = re.compile(r"bn_bwd_(apply|reduce)_multi_kernel<\d+, true")
+    missing = sorted(k for k in _kernels(bench_step, BN_FUSE_ABI) - _kernels(rec.calls, BN_FUSE_ABI)
+                     if not resbn.match(k))
     assert not missing, missing
 
 

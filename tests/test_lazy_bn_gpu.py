@@ -193,7 +193,14 @@ def test_resbn_shortcut_equals_stored(shape, monkeypatch):
     input gradient from bn3's backward kernels), the Bottleneck's LazyBN bn1 and bn3's ReLU
     mask bytes against the stored path: forward bit-identical, gradients and running
     statistics within fp32 summation-order noise."""
-    ba, xa, ya = _bottleneck_run((True, True), monkeypatch, shape)
+    from test_bench_instances_gpu import Recorder
+    with Recorder() as rec:
+        ba, xa, ya = _bottleneck_run((True, True), monkeypatch, shape)
+    names = {k for _, _, ks in rec.calls for k in ks}
+    # bn3's backward kernels specialised for the residual BatchNorm (RB = true) ran
+    import re
+    for rx in (r"bn_bwd_reduce_multi_kernel<\d+, true>", r"bn_bwd_apply_multi_kernel<\d+, true, "):
+        assert any(re.match(rx, k) for k in names), (rx, sorted(names))
     bb, xb, yb = _bottleneck_run((False, False), monkeypatch, shape)
     assert torch.equal(ya, yb)
     assert rel_nz(xa.grad, xb.grad) < 1e-5

@@ -119,6 +119,7 @@ struct IGemm {
   float* stats;  // [2][gridDim.x][n] or null
   int vec_out;   // y 16-byte aligned, y_ps % 4 == 0, no statistics with beta != 0
   FastDiv hw_div, w_div;  // divide by g_h*g_w, g_w
+  int ktab;               // use the K-step table (set_tune key 12, default on)
   // Strided data gradient: one launch covers every stride-parity class of the input
   // pixels, class = blockIdx.z (gridDim.z == 1: the fields above are used as they are).
   struct Cls {
@@ -135,6 +136,8 @@ struct IGemm {
 // column tile: every lane already holds its A fragment (pixel r, 4 channels of the chunk),
 // multiplies it with the remainder rows' weights for those channels, and the 4 lane
 // groups' K shares are summed at the end (dconv3_kernel's remainder, for the gather GEMM).
+constexpr int kIgTab = 1024;  // igemm K-step table entries (16 KB of LDS)
+
 template <int TM, int TN, bool VEC, int ROLE, int KS = 1, bool BF = false, int NR = 0>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   IGemm p = pin;
@@ -193,6 +196,38 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   int tt = 0, c0 = 4 * g + (KS == 1 ? 0 : 16 * wave);
   while (c0 >= p.a_c4) { c0 -= p.a_c4; ++tt; }
   const bool cpad = (p.a_c & 3) != 0;
+  // K-step table (quad step k = (tap, quad) of the linear K order): the tap decode (a
+  // division by ntw), the carry loop and the tap's A / B offsets computed once per
+  // workgroup instead of per lane and chunk; entry = (dh, dw | c0 << 16, weight byte
+  // offset, A element offset (dh * a_w + dw) * a_ps + c0).  Steps past K (the prefetch of
+  // the chunk pairs) get dh far outside the image and kOOB weights: zero operands.
+  __shared__ int4 ktab[kIgTab];
+  const int nq = K >> 2;                                  // quad steps
+  // entries the loop can read: every wave's chunks + the 2 prefetched past its last
+  const int nqt = 4 * ((K + 15) >> 4) + 16 * KS + 16;
+  const bool use_tab = !BF && p.ktab && nqt <= kIgTab;
+  if (use_tab) {
+    const int q4 = p.a_c4 >> 2;
+    for (int k = threadIdx.x; k < nqt; k += 256) {
+      int4 e;
+      if (k < nq) {
+        const int t = k / q4, q = k - t * q4;
+        const int th = t / p.ntw, tw = t - th * p.ntw;
+        const int dh = p.dh0 + th * p.dhs, dw = p.dw0 + tw * p.dws;
+        const int tlin = (p.kh0 + th * p.khs) * p.ksz + (p.kw0 + tw * p.kws);
+        e = make_int4(dh, (dw & 0xffff) | (4 * q) << 16, (int)((uint32_t)(tlin * p.a_c4 + 4 * q) * 4u),
+                      (dh * p.a_w + dw) * p.a_ps + 4 * q);
+      } else {
+        e = make_int4(1 << 20, 0, (int)kOOB, 0);
+      }
+      ktab[k] = e;
+    }
+  }
+  __syncthreads();
+  int kq = g + (KS == 1 ? 0 : 4 * wave);  // this lane's next quad step (as c0 / tt above)
+  int rbase[TM];  // rpix * a_ps: the row's pixel in elements
+#pragma unroll
+  for (int i = 0; i < TM; ++i) rbase[i] = rpix[i] * p.a_ps;
 
   f4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
   f4 fr0[NR > 0 ? NR : 1], fr1[NR > 0 ? NR : 1];  // remainder weights of the chunk
@@ -203,6 +238,35 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   auto load = [&](f4* fa, f4* fb, f4* fr, int& mk) {
+    if (use_tab) {
+      const int4 e = ktab[kq];
+      kq += 4 * KS;
+      const int dh = e.x, dw = (int)(short)(e.y & 0xffff), cq = e.y >> 16;
+      const uint32_t woff = (uint32_t)e.z;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = load4(wrsrc, wrow[j] + woff);
+#pragma unroll
+      for (int q = 0; q < NR; ++q) fr[q] = load4(wrsrc, woff == kOOB ? kOOB : wrowr[q] + woff);
+      const bool m1 = cq + 1 < p.a_c, m2 = cq + 2 < p.a_c, m3 = cq + 3 < p.a_c;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ih = ri[i] + dh, iw = rj[i] + dw;
+        const bool ok = rok[i] && (unsigned)ih < (unsigned)p.a_h && (unsigned)iw < (unsigned)p.a_w;
+        const uint32_t off = ok ? (uint32_t)(rbase[i] + e.w) * 4u : kOOB;
+        f4 v;
+        if (VEC) {
+          v = load4(arsrc, off);
+        } else {
+          v[0] = load1(arsrc, off);
+          v[1] = load1(arsrc, m1 ? off + 4u : kOOB);
+          v[2] = load1(arsrc, m2 ? off + 8u : kOOB);
+          v[3] = load1(arsrc, m3 ? off + 12u : kOOB);
+        }
+        fa[i] = v;
+      }
+      mk = (m1 ? 2 : 0) | (m2 ? 4 : 0) | (m3 ? 8 : 0);
+      return;
+    }
     const bool tv = tt < ntaps;
     const int tc = tv ? tt : 0;
     const int th = tc / p.ntw;
@@ -1312,11 +1376,12 @@ int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 1
 int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
 int g_wgrad_narrow = 1;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
                           // (0 off, 1 on, 2 on with register prefetch)
+int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-step table
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
-    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow;
+    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -1471,6 +1536,7 @@ static void launch_tm(const IGemm& p, const Tile& t, dim3 grid, hipStream_t s) {
 
 // ncls > 1: p.cls[0..ncls) hold the parity classes; the grid covers the largest one.
 int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls) {
+  p.ktab = g_igemm_tab;
   int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
   if (ncls > 1) {
     M = 0;
@@ -2755,6 +2821,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels
     const int prev = g_dconv_stream;
     g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
+    return prev;
+  }
+  if (key == 12) {  // gather GEMM: K-step table (1) or per-chunk tap arithmetic (0)
+    const int prev = g_igemm_tab;
+    g_igemm_tab = value ? 1 : 0;
     return prev;
   }
   if (key == 11) {  // dconv_stream.hip: 18-channel weights in LDS (B operand) or global
