@@ -174,16 +174,23 @@ def _graph_work(port, q):
             return loss
         return step, opt
 
+    def mark(what):
+        sys.stderr.write(f"[rccl graph worker] {what}\n")
+        sys.stderr.flush()
+
     step, opt = make()
     eager = [float(step()) for _ in range(5)]
     torch.cuda.synchronize()
+    mark("eager steps done")
     p_eager = torch.cat([f.data for f in opt.flats]).cpu()
     step, opt = make()
     graph = StepGraph(step, warmup=2)
+    mark("captured")
     replay = []
     for _ in range(3):
         replay.append(float(graph.replay()))
     torch.cuda.synchronize()
+    mark("replayed")
     p_graph = torch.cat([f.data for f in opt.flats]).cpu()
     q.put(("ok", eager, replay, bool(torch.equal(p_eager, p_graph)),
            float((p_eager - p_graph).abs().max())))
@@ -209,11 +216,19 @@ def test_rccl_world1_graph_capture_equals_eager():
     p = ctx.Process(target=_graph_worker, args=(_port(), q))
     p.start()
     import queue
-    try:
-        res = q.get(timeout=200)
-    except queue.Empty:
-        p.kill()
-        pytest.fail(f"captured RCCL step did not report (exit code {p.exitcode})")
+    import sys
+    import time
+    t0, res = time.time(), None
+    while res is None:  # heartbeat on the real stderr: a silent wait looks like a hang
+        try:
+            res = q.get(timeout=15)
+        except queue.Empty:
+            waited = time.time() - t0
+            sys.__stderr__.write(f"[rccl graph test] waiting for the worker ({waited:.0f} s)\n")
+            sys.__stderr__.flush()
+            if waited > 200 or not p.is_alive():
+                p.kill()
+                pytest.fail(f"captured RCCL step did not report (exit code {p.exitcode})")
     p.join(timeout=60)
     assert res[0] == "ok", res[1]
     _, eager, replay, same, maxdiff = res
