@@ -429,6 +429,11 @@ def flush_wgrad(own_stream=False):
     cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
     if own_stream:
         key = cur.cuda_stream if cur is not None else None
+        # a full flush earlier in this backward may have launched reductions this stream
+        # queued on another stream: whatever follows here (vae2.dist.anchor_reduce's
+        # all-reduce) is ordered after them
+        if _FLUSH_EV[0] is not None and cur is not None:
+            cur.wait_event(_FLUSH_EV[0])
         call("vae2_wgrad_flush_stream", stream_ptr())
         keep = [(k, t_) for k, t_ in _WS_HOLD if k != key]
         _WS_HOLD[:] = keep
@@ -441,12 +446,21 @@ def flush_wgrad(own_stream=False):
             for _, t_ in _WS_HOLD:
                 if t_.is_cuda:
                     t_.record_stream(cur)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            _FLUSH_EV[0] = ev
         _WS_HOLD.clear()
+
+
+# completion of the last full flush of the current backward on its launch stream (reset at
+# the end of every backward, so a wait never spans steps or a graph capture's boundary)
+_FLUSH_EV = [None]
 
 
 def _end_of_backward():
     _WGRAD_CB[0] = False
     flush_wgrad()
+    _FLUSH_EV[0] = None
 
 
 def _graph_task():
