@@ -14,11 +14,12 @@ variant; the same step with fp32 operands keeps the fp32 bounds):
               trajectory is chaotic: Adam's first steps move every weight by ~lr;
               measured deviation <= 7 %).
 Per-tensor gradients (test_bf16_config2_per_tensor_gradients_track_fp32): on a
-Kaiming-scale state, against the fp32-operand HIP step, cosine >= 0.99 and norm within
-5 % on the tensors the reference's own fp64 step holds under a bf16-sized input
-perturbation (the output heads); the rest of this BatchNorm network's gradient is
-chaotic in its inputs in the reference's arithmetic too (tests/diag_grad_chaos.py), so
-there only the norm is bounded."""
+Kaiming-scale state, against the fp32-operand HIP step, on the 16 tensors the
+reference's own fp64 step holds under a bf16-sized input perturbation (the output heads):
+median cosine >= 0.99, every cosine >= 0.98, every norm within 10 %; the rest of this
+BatchNorm network's gradient is chaotic in its inputs in the reference's arithmetic too
+(tests/diag_grad_chaos.py), so there only the median norm ratio is bounded, to [0.5, 2]
+(a loose bound: it catches a missing or doubled gradient, not a wrong direction)."""
 import pytest
 import torch
 
