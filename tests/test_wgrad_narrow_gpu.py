@@ -83,6 +83,11 @@ def test_wgrad_narrow_matches_fp64(shape):
     # the register-prefetch form (tune key 7 = 2) computes the same sums in the same order
     dw_pf, _ = _run(x, dy, 2)
     assert torch.equal(dw, dw_pf)
+    # the 8-wave form (key 7 = 3: the extra waves split the pixel chunks, summed through
+    # LDS in wave order): the same sums in another order
+    dw_8, names_8 = _run(x, dy, 3)
+    assert any(k.startswith("wgrad3n_kernel") and k.endswith(", 8>") for k in names_8), names_8
+    assert rel(dw_8, dw) < 1e-5
 
 
 @pytest.mark.parametrize("shape", [(8, 128, 256, 18, 0), (2, 13, 37, 36, 4), (1, 6, 40, 72, 0)])

@@ -1374,8 +1374,9 @@ int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients ov
 int g_gemm1_tn = 4;
 int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 16 * TM pixels (1, 2)
 int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
-int g_wgrad_narrow = 1;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
-                          // (0 off, 1 on, 2 on with register prefetch)
+int g_wgrad_narrow = 3;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
+                          // (0 off, 1 on, 2 on with register prefetch, 3 on with 8 waves:
+                          //  18 / 36 / 72 ch 35.0 / 31.7 / 32.1 -> 33.0 / 31.4 / 31.2 us)
 int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-step table
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
@@ -2815,7 +2816,7 @@ int vae2_conv2d_set_tune(int key, int value) {
   }
   if (key == 7) {
     const int prev = g_wgrad_narrow;
-    g_wgrad_narrow = value >= 0 && value <= 2 ? value : 1;
+    g_wgrad_narrow = value >= 0 && value <= 3 ? value : 1;
     return prev;
   }
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels

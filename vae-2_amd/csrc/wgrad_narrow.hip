@@ -53,8 +53,10 @@ struct WGN {
 // MFMA; NR: remainder co rows on the VALU (<= 4, one staged quad); WPIX: waves splitting the
 // pixels of a tile (1, 2 or 4); PF: the next tile's loads in registers during the current
 // tile's MFMAs (else the resident workgroups of a CU overlap each other's staging).
-template <int CQ, int TM, int NR, int WPIX, bool PF>
-__global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
+// NW: waves per workgroup (4, or 8: twice the waves per SIMD for the same tiles and partial
+// slabs, the extra waves splitting the pixel chunks -- set_tune key 7 = 3)
+template <int CQ, int TM, int NR, int WPIX, bool PF, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
   constexpr int CSW = 4 * CQ;
   constexpr int CO = 16 * TM + NR;
   constexpr int COQ = (CO + 3) / 4;
@@ -62,10 +64,11 @@ __global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
   constexpr int XP = CSW;                        // X floats per halo pixel in LDS
   constexpr int LPX = (kTH + 2) * kLW;           // halo pixels
   constexpr int G = (3 * CSW + 15) / 16;         // 16-column groups per dw
-  constexpr int WCOL = 4 / WPIX;
+  constexpr int WCOL = NW / WPIX;
+  constexpr int NT = 64 * NW;
   constexpr int GW = (G + WCOL - 1) / WCOL;      // groups per wave
   static_assert(NR <= 4 && (NR == 0 || COQ == 4 * TM + 1), "one remainder quad");
-  static_assert(WPIX == 1 || WPIX == 2 || WPIX == 4, "waves per tile");
+  static_assert(WCOL * WPIX == NW && (WCOL == 1 || WCOL == 2 || WCOL == 4), "waves per tile");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* xs = sm;                   // [LPX][XP]
   float* ds = sm + LPX * XP;        // [kNPX][DP]
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(256) void wgrad3n_kernel(WGN p) {
   const int te = tb + p.tps < p.ntiles ? tb + p.tps : p.ntiles;
   // staging map: thread -> one channel quad (fixed) and pixels b, b + XPU, b + 2 XPU, ...
   // (no per-item division by the quad count)
-  constexpr int XPU = 256 / CQ, DPU = 256 / COQ;  // pixels per pass
+  constexpr int XPU = NT / CQ, DPU = NT / COQ;  // pixels per pass
   constexpr int NXI = (LPX + XPU - 1) / XPU, NDI = (kNPX + DPU - 1) / DPU;
   const int xq = threadIdx.x % CQ, xb = threadIdx.x / CQ;     // xb < XPU: active
   const int dq = threadIdx.x % COQ, db = threadIdx.x / COQ;
@@ -338,6 +341,7 @@ namespace {
 struct Cfg {
   int cq, tm, nr, wpix, ci_slabs, co_slabs;
   int pf = 0;
+  int nw = 4;  // waves per workgroup
 };
 
 // 18 = 16 + 2 (one ci slab of 5 quads; 2 waves per column half of the tile's chunks); 36 = 32 + 4 (9 quads); 72 = 2 co slabs x (32 + 4),
@@ -349,19 +353,26 @@ bool pick(const vae2_act* xd, const vae2_act* dyd, Cfg& c) {
   else if (dyd->c == 72) c = Cfg{9, 2, 4, 1, 2, 2};
   else return false;
   c.pf = g_wgrad_narrow == 2;  // (tune key 7 = 2: register prefetch of the next tile)
+  if (g_wgrad_narrow == 3) {    // (key 7 = 3: 8 waves, the extra 4 splitting the pixels)
+    c.nw = 8;
+    c.wpix *= 2;
+  }
   return true;
 }
 
 size_t lds_bytes(const Cfg& c) {
   const int CO = 16 * c.tm + c.nr, DP = 4 * ((CO + 3) / 4);
   const size_t stage = ((size_t)(kTH + 2) * kLW * 4 * c.cq + (size_t)kNPX * DP) * sizeof(float);
-  const int G = (3 * 4 * c.cq + 15) / 16, wcol = 4 / c.wpix, gw = (G + wcol - 1) / wcol;
+  const int G = (3 * 4 * c.cq + 15) / 16, wcol = c.nw / c.wpix, gw = (G + wcol - 1) / wcol;
   const size_t nv = (size_t)c.tm * gw * 12 + (size_t)gw * 3 * c.nr;
   const size_t red = c.wpix > 1 ? (size_t)(c.wpix - 1) * wcol * nv * 64 * sizeof(float) : 0;
   return stage > red ? stage : red;
 }
 
 const void* kernel_of(const Cfg& c) {
+  if (c.nw == 8)
+    return c.cq == 5 ? reinterpret_cast<const void*>(wgrad3n_kernel<5, 1, 2, 4, false, 8>)
+                     : reinterpret_cast<const void*>(wgrad3n_kernel<9, 2, 4, 2, false, 8>);
   if (c.cq == 5) return c.pf ? reinterpret_cast<const void*>(wgrad3n_kernel<5, 1, 2, 2, true>)
                              : reinterpret_cast<const void*>(wgrad3n_kernel<5, 1, 2, 2, false>);
   return c.pf ? reinterpret_cast<const void*>(wgrad3n_kernel<9, 2, 4, 1, true>)
@@ -369,11 +380,11 @@ const void* kernel_of(const Cfg& c) {
 }
 
 int resident_per_cu(const Cfg& c) {
-  static int cache[4] = {0, 0, 0, 0};
-  const int k = (c.cq == 5 ? 0 : 1) + 2 * c.pf;
+  static int cache[6] = {0, 0, 0, 0, 0, 0};
+  const int k = (c.cq == 5 ? 0 : 1) + (c.nw == 8 ? 4 : 2 * c.pf);
   if (!cache[k]) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_of(c), 256, lds_bytes(c)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_of(c), 64 * c.nw, lds_bytes(c)) !=
             hipSuccess || n < 1) {
       (void)hipGetLastError();
       n = 1;
@@ -433,10 +444,12 @@ int wgrad3n_launch(const float* x, const vae2_act* xd, const float* dy, const va
   dim3 grid((unsigned)pl.splits, (unsigned)(pl.c.ci_slabs * pl.c.co_slabs));
   const size_t shm = lds_bytes(pl.c);
   if (pl.c.cq == 5) {
-    if (pl.c.pf) VAE2_LAUNCH((wgrad3n_kernel<5, 1, 2, 2, true>), grid, dim3(256), shm, s, p);
+    if (pl.c.nw == 8) VAE2_LAUNCH((wgrad3n_kernel<5, 1, 2, 4, false, 8>), grid, dim3(512), shm, s, p);
+    else if (pl.c.pf) VAE2_LAUNCH((wgrad3n_kernel<5, 1, 2, 2, true>), grid, dim3(256), shm, s, p);
     else VAE2_LAUNCH((wgrad3n_kernel<5, 1, 2, 2, false>), grid, dim3(256), shm, s, p);
   } else {
-    if (pl.c.pf) VAE2_LAUNCH((wgrad3n_kernel<9, 2, 4, 1, true>), grid, dim3(256), shm, s, p);
+    if (pl.c.nw == 8) VAE2_LAUNCH((wgrad3n_kernel<9, 2, 4, 2, false, 8>), grid, dim3(512), shm, s, p);
+    else if (pl.c.pf) VAE2_LAUNCH((wgrad3n_kernel<9, 2, 4, 1, true>), grid, dim3(256), shm, s, p);
     else VAE2_LAUNCH((wgrad3n_kernel<9, 2, 4, 1, false>), grid, dim3(256), shm, s, p);
   }
   const hipError_t e = hipGetLastError();
