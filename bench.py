@@ -232,6 +232,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # = vae2.dist.prepare_nccl_env
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

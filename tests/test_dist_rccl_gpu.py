@@ -52,6 +52,7 @@ def _work(port, q):
     ref = refs[0]
     base_same = bool(torch.equal(refs[0][2], refs[1][2]))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # vae2.dist.prepare_nccl_env
     dist.init_process_group("nccl", rank=0, world_size=1)
     assert dist.get_backend() == "nccl"
     vdist.FORCE = True  # the distributed path at world size 1
@@ -151,6 +152,7 @@ def _graph_work(port, q):
     torch.cuda.set_device(0)
     g = golden("tiny_native")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # vae2.dist.prepare_nccl_env
     dist.init_process_group("nccl", rank=0, world_size=1)
     vdist.FORCE = True
     vdist.set_sync_bn(True)

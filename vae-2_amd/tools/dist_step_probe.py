@@ -37,6 +37,8 @@ def main():
     torch.cuda.set_device(0)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
+    from vae2.dist import prepare_nccl_env
+    prepare_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1)
     vdist.FORCE = True
     vdist.set_sync_bn(True)

@@ -56,6 +56,7 @@ def init(backend=None):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        prepare_nccl_env()
     dist.init_process_group(backend=backend, init_method="env://")
 
 
@@ -142,6 +143,14 @@ def init_syncbn_ipc(group=None, max_elems=SB_MAX_ELEMS):
 
 
 FORCE_IPC = False  # tests: the IPC exchange under a gloo group (ranks sharing one GPU)
+
+
+def prepare_nccl_env():
+    """Environment for a NCCL (RCCL) process group whose steps are captured as HIP graphs:
+    ProcessGroupNCCL's CUDA-event cache off (an event of an eager collective must never be
+    re-recorded inside a capture while the watchdog may still query it).  Call before
+    torch.distributed.init_process_group; an explicit setting wins."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def syncbn_exchange():

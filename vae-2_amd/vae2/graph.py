@@ -20,8 +20,16 @@ earlier (eager, warm-up) collectives with hipEventQuery; under the default globa
 mode HIP refuses that call from any thread while a capture is open
 (hipErrorStreamCaptureUnsupported), the watchdog thread dies and aborts the process
 (observed on MI355X with a world-size-1 RCCL group; round 4 saw the same capture
-hang).  Thread-local mode restricts only the capturing thread.
+hang).  Thread-local mode restricts only the capturing thread.  Before capturing, the
+warm-up collectives are drained: the GPU is synchronised and the watchdog (which polls
+every 100 ms) is given time to retire them, so it holds no work whose events it still
+queries while the capture is open (a watchdog query that met an event recorded in the
+capturing stream aborted one run of the world-1 test: hipErrorCapturedEvent); callers
+also disable ProcessGroupNCCL's event cache (`vae2.dist.prepare_nccl_env`), so no event
+of an eager collective is re-recorded by a captured one.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -48,6 +56,8 @@ class StepGraph:
             streams.join_all()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if capture_error_mode == "thread_local":
+            time.sleep(0.5)  # the NCCL watchdog retires the warm-up collectives first
         self.graph = torch.cuda.CUDAGraph()
         streams._FORKED.clear()
         try:
