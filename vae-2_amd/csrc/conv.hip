@@ -1378,11 +1378,12 @@ int g_wgrad_narrow = 3;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18
                           // (0 off, 1 on, 2 on with register prefetch, 3 on with 8 waves:
                           //  18 / 36 / 72 ch 35.0 / 31.7 / 32.1 -> 33.0 / 31.4 / 31.2 us)
 int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-step table
+int g_dconv_n16 = 0;      // vae2_conv2d_set_tune key 13: direct 3x3 16-channel N blocks when short of workgroups
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
-    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab;
+    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab, g_dconv_n16;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2389,6 +2390,14 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   if (d.nr && g_conv_algo != 2 && ad->n * d.tiles_h * d.tiles_w < 512) {
     d.tn = t.tn; d.nblk = t.nblk; d.nr = 0;
   }
+  // tune key 13: a layer whose tiles leave fewer than 2 workgroups per CU (the 72-channel
+  // branch at 32 x 64: 256 workgroups = one wave per SIMD) takes 16-channel N blocks --
+  // more workgroups re-staging the same halo tile (L2-resident) for more waves per SIMD
+  if (g_dconv_n16 && !g_bf16 && d.nr == 0 && d.tn > 1 && N > 16 &&
+      ad->n * d.tiles_h * d.tiles_w * d.nblk < 512) {
+    d.tn = 1;
+    d.nblk = (N + 15) / 16;
+  }
   return d;
 }
 
@@ -2822,6 +2831,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels
     const int prev = g_dconv_stream;
     g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
+    return prev;
+  }
+  if (key == 13) {  // direct 3x3: 16-channel N blocks for layers short of workgroups
+    const int prev = g_dconv_n16;
+    g_dconv_n16 = value ? 1 : 0;
     return prev;
   }
   if (key == 12) {  // gather GEMM: K-step table (1) or per-chunk tap arithmetic (0)
