@@ -1373,7 +1373,8 @@ int g_wgrad_nw8 = 1;      // vae2_conv2d_set_tune key 3: 3x3 weight gradients ov
 // 153 -> 127 us; step 845.1 / 845.4 (8) vs 847.3 / 848.0 frames/s (4), same box.
 int g_gemm1_tn = 4;
 int g_gemm1_tm = 2;       // vae2_conv2d_set_tune key 5: 1x1 GEMM row tiles of 16 * TM pixels (1, 2)
-int g_igemm_nr = 0;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36
+int g_igemm_nr = 2;       // vae2_conv2d_set_tune key 6: igemm VALU remainder for N = 18 / 36 (1),
+                          // N = 18 only (2, default: step 895.7 -> 899.8 frames/s, 3 A/B pairs)
 int g_wgrad_narrow = 3;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18 / 36 / 72 channels
                           // (0 off, 1 on, 2 on with register prefetch, 3 on with 8 waves:
                           //  18 / 36 / 72 ch 35.0 / 31.7 / 32.1 -> 33.0 / 31.4 / 31.2 us)
@@ -1425,8 +1426,9 @@ static Tile pick_igemm_tile(int64_t M, int N, int taps, int k4, int ncls) {
   const int64_t blocks = ceil_div(M, 64 * t.tm) * t.nblk * ncls;
   const int chunks = (taps * k4 + 15) / 16;
   if (g_ksplit && !wide && blocks < 512 && chunks >= 16) t.ks = 4;
-  // tune key 6: 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder, fp32, no K split)
-  if (g_igemm_nr && !g_bf16 && t.ks == 1 && !wide && (N == 18 || N == 36)) {
+  // tune key 6: 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder, fp32, no K split);
+  // 2: 18 channels only
+  if (g_igemm_nr && !g_bf16 && t.ks == 1 && !wide && (N == 18 || (N == 36 && g_igemm_nr == 1))) {
     t.tn = N == 18 ? 1 : 2;
     t.nr = N == 18 ? 2 : 4;
     t.nblk = 1;
@@ -2815,7 +2817,7 @@ int vae2_conv2d_set_tune(int key, int value) {
   }
   if (key == 6) {
     const int prev = g_igemm_nr;
-    g_igemm_nr = value ? 1 : 0;
+    g_igemm_nr = value >= 0 && value <= 2 ? value : 0;
     return prev;
   }
   if (key == 8) {  // bn.hip: buffer-resource BatchNorm bodies
