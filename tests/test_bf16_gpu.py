@@ -96,10 +96,21 @@ def test_bf16_config2_forward_against_fp32_oracle():
 
 
 def test_bf16_config2_training_tracks_fp32():
+    """(The fp32 reference run uses the kernel forms the bf16 run uses: with bf16 operands
+    the gather kernel never takes its 18-channel VALU-remainder form (set_tune key 6), and
+    Adam's first steps turn any summation-order difference into a different trajectory --
+    the fp32 run alone moves 5 % at step 1 between key 6 = 0 and 2 -- so the comparison
+    isolates the operand rounding.)"""
+    from vae2 import _lib
     xs, eps, code = _inputs()
     xs = [0.1 * x for x in xs]
-    h32, _ = _run(False, xs, eps, code, steps=6, lr=3e-3)
-    h16, _ = _run(True, xs, eps, code, steps=6, lr=3e-3)
+    lib = _lib.load()
+    prev6 = lib.vae2_conv2d_set_tune(6, 0)
+    try:
+        h32, _ = _run(False, xs, eps, code, steps=6, lr=3e-3)
+        h16, _ = _run(True, xs, eps, code, steps=6, lr=3e-3)
+    finally:
+        lib.vae2_conv2d_set_tune(6, prev6)
     assert abs(h16[0][0] - h32[0][0]) <= 2e-3 * h32[0][0]
     for i, (a, b) in enumerate(zip(h16, h32)):
         assert abs(a[0] - b[0]) <= 0.15 * abs(b[0]), (i, a[0], b[0])
