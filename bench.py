@@ -98,6 +98,9 @@ def parse():
                     help="the reference's full training iteration (function.py:443-512): "
                          "GAN_LAMBDA 1 (both LSGAN generator terms through the two "
                          "discriminators) + the discriminator step with its own Adam")
+    ap.add_argument("--level-lanes", type=int, default=None,
+                    help="concurrent streams per HRNet depth level inside the captured graph "
+                         "(vae2.ops.LEVEL_LANES; 0/1: one stream)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto = on, at every world "
                          "size: the distributed step's RCCL collectives are captured in "
@@ -233,6 +236,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # = vae2.dist.prepare_nccl_env
+        if "TORCH_NCCL_TRACE_BUFFER_SIZE" not in os.environ:  # flight recorder: the graph
+            os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2000")  # capture's drain reads it
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -262,7 +267,10 @@ def main():
         from vae2 import _lib
         k, v = kv.split("=")
         if _lib.load().vae2_conv2d_set_tune(int(k), int(v)) < 0:
-            raise SystemExit(f"unknown conv tune key {k}")
+            raise SystemExit(f"conv tune key {k}: unknown key or out-of-range value {v}")
+    if args.level_lanes is not None:
+        from vae2 import ops as vops
+        vops.LEVEL_LANES = args.level_lanes
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False

@@ -32,7 +32,7 @@ typedef struct vae2_act {
   int64_t ps; /* pixel stride, in elements */
 } vae2_act;
 
-#define VAE2_ABI_VERSION 11
+#define VAE2_ABI_VERSION 12
 
 int vae2_abi_version(void);
 const char* vae2_last_error(void);
@@ -79,7 +79,8 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * 18 / 36 / 72-channel 3x3 weight gradients spread their column tiles over 8 waves;
  * key 4 = the persistent 1x1 GEMM's maximum N tiles (of 16 channels) per workgroup, 3..8
  * (default 4); key 5 = 1: its row tiles of 16 instead of 32 pixels; key 6 = 1: gather-GEMM
- * convs with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder columns).  Returns the previous value, -1 for an unknown key.                      */
+ * convs with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder columns).  Returns the previous value, -1 for an unknown key or an
+ * out-of-range value of keys 4, 6 and 7 (the setting is then left unchanged).          */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab
@@ -646,8 +647,13 @@ int vae2_scale(float* dst, const float* src, int64_t n, float scale,
  * (vae2_syncbn_comm_bytes) and writes its 64-byte IPC handle; the handles of all ranks,
  * concatenated in rank order, go to vae2_syncbn_comm_connect.  n <= max_elems doubles
  * per call; the calls are stream-ordered and must be made in the same order on every
- * rank (a HIP graph may capture them).  Waits are bounded (60 s): a missing peer sets the
- * error word (vae2_syncbn_comm_error, a synchronous read) instead of hanging.  world <= 8. */
+ * rank (a HIP graph may capture them).  Waits are bounded (60 s by default,
+ * vae2_syncbn_comm_set_timeout): a missing peer sets the error word (vae2_syncbn_comm_error,
+ * a synchronous read) instead of hanging.  ABI 12: a failure is sticky and visible in the
+ * data -- the timed-out exchange and every later one on this comm write NaN into buf and
+ * exchange nothing (no payload, no flag), so the statistics turn NaN and the step's NaN/Inf
+ * checks fire even where the error word is never read.  The receive areas are uncached
+ * device memory.  world <= 8.                                                              */
 typedef struct vae2_syncbn_comm vae2_syncbn_comm;
 int64_t vae2_syncbn_comm_bytes(int world, int64_t max_elems);
 int vae2_syncbn_comm_init(int rank, int world, int64_t max_elems, void* handle_out,
@@ -655,6 +661,7 @@ int vae2_syncbn_comm_init(int rank, int world, int64_t max_elems, void* handle_o
 int vae2_syncbn_comm_connect(vae2_syncbn_comm* comm, const void* handles);
 int vae2_syncbn_allreduce(vae2_syncbn_comm* comm, double* buf, int64_t n, void* stream);
 int vae2_syncbn_comm_error(vae2_syncbn_comm* comm, int64_t* host_out);
+int vae2_syncbn_comm_set_timeout(vae2_syncbn_comm* comm, double seconds);
 int vae2_syncbn_comm_destroy(vae2_syncbn_comm* comm);
 
 #ifdef __cplusplus

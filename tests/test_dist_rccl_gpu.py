@@ -52,7 +52,7 @@ def _work(port, q):
     ref = refs[0]
     base_same = bool(torch.equal(refs[0][2], refs[1][2]))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # vae2.dist.prepare_nccl_env
+    vdist.prepare_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1)
     assert dist.get_backend() == "nccl"
     vdist.FORCE = True  # the distributed path at world size 1
@@ -146,13 +146,14 @@ def _graph_work(port, q):
     import torch.distributed as dist
     from helpers import build, golden, make_cfg, t
     from vae2 import dist as vdist
+    from vae2 import graph as vgraph
     from vae2.graph import StepGraph
     from vae2.model import FullModel_encdec
     from vae2.optim import FusedAdam
     torch.cuda.set_device(0)
     g = golden("tiny_native")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # vae2.dist.prepare_nccl_env
+    vdist.prepare_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1)
     vdist.FORCE = True
     vdist.set_sync_bn(True)
@@ -186,8 +187,12 @@ def _graph_work(port, q):
     mark("eager steps done")
     p_eager = torch.cat([f.data for f in opt.flats]).cpu()
     step, opt = make()
+    # the eager steps' collectives are all visible to the drain (flight recorder on) ...
+    n_eager = len(vgraph.pending_collectives()) + 0
     graph = StepGraph(step, warmup=2)
-    mark("captured")
+    # ... and none was left un-retired when the capture opened
+    drained = vgraph.pending_collectives() == [] and not any(vdist._EARLY.values())
+    mark(f"captured (drain polls {graph.drain_polls}, pending before the warm-up {n_eager})")
     replay = []
     for _ in range(3):
         replay.append(float(graph.replay()))
@@ -195,7 +200,7 @@ def _graph_work(port, q):
     mark("replayed")
     p_graph = torch.cat([f.data for f in opt.flats]).cpu()
     q.put(("ok", eager, replay, bool(torch.equal(p_eager, p_graph)),
-           float((p_eager - p_graph).abs().max())))
+           float((p_eager - p_graph).abs().max()), drained))
     dist.destroy_process_group()
 
 
@@ -233,7 +238,8 @@ def test_rccl_world1_graph_capture_equals_eager():
                 pytest.fail(f"captured RCCL step did not report (exit code {p.exitcode})")
     p.join(timeout=60)
     assert res[0] == "ok", res[1]
-    _, eager, replay, same, maxdiff = res
+    _, eager, replay, same, maxdiff, drained = res
     print(f"eager {eager}, replay {replay}, params identical {same} (max |diff| {maxdiff:.3g})")
+    assert drained, "eager collectives were still held by the NCCL watchdog at capture"
     assert replay == eager[2:], (replay, eager)
     assert same, maxdiff

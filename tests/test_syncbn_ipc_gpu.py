@@ -146,3 +146,93 @@ def test_syncbn_ipc_two_ranks_exact_sums():
               f"(eager issue), {usg:.1f} us per exchange in a replayed graph")
         assert ok, "eager exchanges differ from the rank-order sums"
         assert gok, "graph-replayed exchanges wrong"
+
+
+def _fail_work(rank, world, port, q):
+    """Failure semantics of the exchange (ABI 12): a late peer and diverged exchange
+    sequences fail loudly, stickily and with NaN statistics -- never a silent local sum."""
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "vae-2_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from vae2 import dist as vdist
+    vdist.FORCE_IPC = True
+    vdist.set_sync_bn(True)
+    out = {}
+    # (1) a late peer: rank 1 arrives at exchange 2 after rank 0's bound (0.3 s) expired
+    assert vdist.init_syncbn_ipc(dist.group.WORLD), "IPC exchange did not come up"
+    vdist._SB.set_timeout(0.3)
+    res = []
+    for k in range(3):
+        if k == 1 and rank == 1:
+            time.sleep(1.5)
+        t = torch.full((64,), float(rank + 1), dtype=torch.float64, device="cuda")
+        vdist.syncbn_all_reduce_(t)
+        torch.cuda.synchronize()
+        res.append(t.cpu())
+    out["late"] = [(bool(torch.isnan(r).all()), float(r[0])) for r in res]
+    try:
+        vdist.syncbn_check()
+        out["late_raised"] = False
+    except vdist.SyncBNExchangeError:
+        out["late_raised"] = True
+    dist.barrier()
+    # (2) diverged sequences: same exchange number, different payload lengths
+    assert vdist.init_syncbn_ipc(dist.group.WORLD), "second IPC comm did not come up"
+    vdist._SB.set_timeout(5.0)
+    t = torch.ones(10 + 2 * rank, dtype=torch.float64, device="cuda")
+    vdist.syncbn_all_reduce_(t)
+    torch.cuda.synchronize()
+    out["mismatch_nan"] = bool(torch.isnan(t.cpu()).all())
+    out["mismatch_err"] = vdist._SB.error()
+    q.put((rank, "ok", out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _fail_worker(rank, world, port, q):
+    try:
+        _fail_work(rank, world, port, q)
+    except BaseException:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.timeout(300)
+def test_syncbn_ipc_failures_are_sticky_and_nan():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    import queue
+    res, deadline = [], time.time() + 200
+    while len(res) < 2:
+        try:
+            res.append(q.get(timeout=5))
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs) or time.time() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"IPC failure run failed: exit codes {[p.exitcode for p in procs]}")
+    for p in procs:
+        p.join(timeout=60)
+    errors = [r for r in res if r[1] == "error"]
+    assert not errors, errors[0][2]
+    by = {r: o for r, _, o in res}
+    print(by)
+    # exchange 0: exact on both ranks
+    assert by[0]["late"][0] == (False, 3.0) and by[1]["late"][0] == (False, 3.0)
+    # rank 0 waited for rank 1 past its bound: NaN, then sticky NaN (no pairing with
+    # rank 1's late exchange 1 as if it were its exchange 2)
+    assert by[0]["late"][1][0] and by[0]["late"][2][0]
+    # rank 1 found rank 0's exchange-1 payload (rank 0 stored it before waiting): exact; its
+    # exchange 2 then waits for a rank that stopped raising flags: NaN
+    assert by[1]["late"][1] == (False, 3.0) and by[1]["late"][2][0]
+    assert by[0]["late_raised"] and by[1]["late_raised"]
+    for r in (0, 1):
+        assert by[r]["mismatch_nan"] and by[r]["mismatch_err"] != 0

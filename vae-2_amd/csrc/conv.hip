@@ -2806,8 +2806,9 @@ int vae2_conv2d_set_tune(int key, int value) {
     return prev;
   }
   if (key == 4) {
+    if (value < 3 || value > 8) return -1;  // rejected, setting unchanged
     const int prev = g_gemm1_tn;
-    g_gemm1_tn = value >= 3 && value <= 8 ? value : 4;
+    g_gemm1_tn = value;
     return prev;
   }
   if (key == 5) {
@@ -2816,8 +2817,9 @@ int vae2_conv2d_set_tune(int key, int value) {
     return prev;
   }
   if (key == 6) {
+    if (value < 0 || value > 2) return -1;
     const int prev = g_igemm_nr;
-    g_igemm_nr = value >= 0 && value <= 2 ? value : 0;
+    g_igemm_nr = value;
     return prev;
   }
   if (key == 8) {  // bn.hip: buffer-resource BatchNorm bodies
@@ -2826,8 +2828,9 @@ int vae2_conv2d_set_tune(int key, int value) {
     return prev;
   }
   if (key == 7) {
+    if (value < 0 || value > 3) return -1;
     const int prev = g_wgrad_narrow;
-    g_wgrad_narrow = value >= 0 && value <= 3 ? value : 1;
+    g_wgrad_narrow = value;
     return prev;
   }
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels

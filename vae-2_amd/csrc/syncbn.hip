@@ -17,6 +17,18 @@
 // HIP graph replays correctly.  Every wait is bounded (s_memrealtime, 60 s): a missing peer
 // sets the area's error word and the kernel exits instead of hanging the GPU.
 //
+// Failures are sticky and visible in the data: a timed-out exchange writes NaN into the
+// caller's buffer (the statistics become NaN, so the step's NaN/Inf checks see it even
+// where nobody reads the error word), and every later exchange on this comm finds the
+// error word set at entry, copies nothing, raises no flag and writes NaN again -- a rank
+// never goes on pairing its payloads with the wrong exchange of its peers.  The receive
+// areas are uncached device memory (hipDeviceMallocUncached), so the peers' system-scope
+// stores over xGMI and this rank's polling loads meet in HBM, not in a stale L2 line.
+//
+// A flag word is seq | n << 40: a rank whose peer arrived at the same sequence number with
+// a different payload length (the ranks' exchange sequences diverged -- e.g. one rank's
+// control flow skipped a layer) fails that exchange instead of summing unrelated payloads.
+//
 // Area layout (bytes): [0, 64) control {seq, error}; [64, 64 + 16 * world) flags[2][world]
 // (u64); from kRecvOff: recv[2][world][max_elems] doubles.
 #include <hip/hip_runtime.h>
@@ -28,7 +40,8 @@
 struct vae2_syncbn_comm {
   int rank, world;
   int64_t max_elems;
-  void* area;                          // own area (hipMalloc'd here, freed by destroy)
+  uint64_t timeout_ticks;              // s_memrealtime ticks (100 MHz) before giving up
+  void* area;                          // own area (allocated here, freed by destroy)
   void* peers[vae2::kSyncMaxRanks];    // every rank's area mapped in this process
   bool opened[vae2::kSyncMaxRanks];    // peers[r] from hipIpcOpenMemHandle
 };
@@ -42,11 +55,14 @@ constexpr int64_t kRecvOff = 4096;
 // module loading, graph capture; a timed-out exchange corrupts the sequence, so the host
 // checks the error word -- vae2.dist.syncbn_check -- and fails loudly)
 constexpr uint64_t kTimeoutTicks = 6000000000ull;
+constexpr double kTicksPerSecond = 1.0e8;
+constexpr uint64_t kSeqMask = (1ull << 40) - 1;
 
 struct SyncArgs {
   char* peers[kSyncMaxRanks];
   int rank, world;
   int64_t max_elems;
+  uint64_t timeout_ticks;
   double* buf;
   int n;
 };
@@ -60,12 +76,21 @@ __global__ __launch_bounds__(256) void syncbn_allreduce_kernel(SyncArgs p) {
   __shared__ int sfail;
   char* own = p.peers[p.rank];
   if (threadIdx.x == 0) {
-    const uint64_t s = ctrl(own)[0] + 1;  // only this (stream-ordered) kernel writes it
-    ctrl(own)[0] = s;
-    sseq = s;
-    sfail = 0;
+    // sticky failure: an earlier exchange of this comm timed out -> no payload, no flag
+    const uint64_t err = __hip_atomic_load(ctrl(own) + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    sfail = err != 0;
+    if (!sfail) {
+      const uint64_t s = ctrl(own)[0] + 1;  // only this (stream-ordered) kernel writes it
+      ctrl(own)[0] = s;
+      sseq = s;
+    }
   }
   __syncthreads();
+  if (sfail) {
+    for (int i = threadIdx.x; i < p.n; i += blockDim.x) p.buf[i] = __builtin_nan("");
+    return;
+  }
   const uint64_t seq = sseq;
   const int slot = (int)(seq & 1);
   // 1. the payload into every rank's slot (system scope: visible to the peer's loads)
@@ -78,25 +103,30 @@ __global__ __launch_bounds__(256) void syncbn_allreduce_kernel(SyncArgs p) {
   __syncthreads();                                // complete before the flags below
   // 2. arrival flags (thread r raises ours in rank r's area)
   if ((int)threadIdx.x < p.world) {
-    __hip_atomic_store(flags(p.peers[threadIdx.x]) + slot * p.world + p.rank, seq,
-                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(flags(p.peers[threadIdx.x]) + slot * p.world + p.rank,
+                       seq | ((uint64_t)p.n << 40), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 3. wait for every rank's flag in our area (bounded)
+  // 3. wait for every rank's flag in our area (bounded), then check its payload length
   if ((int)threadIdx.x < p.world) {
     uint64_t* f = flags(own) + slot * p.world + threadIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    uint64_t v;
+    bool late = false;
+    while (((v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) & kSeqMask) <
+           seq) {
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
-        sfail = 1;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
+        late = true;
         break;
       }
     }
+    if (late || (v >> 40) != (uint64_t)p.n) sfail = 1;
   }
   __syncthreads();
-  if (sfail) {
+  if (sfail) {  // the statistics of this exchange are undefined: make them NaN
     if (threadIdx.x == 0)
       __hip_atomic_fetch_or(ctrl(own) + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = threadIdx.x; i < p.n; i += blockDim.x) p.buf[i] = __builtin_nan("");
     return;
   }
   // 4. the world payloads in rank order (system-scope loads: the peers wrote them)
@@ -137,8 +167,10 @@ int vae2_syncbn_comm_init(int rank, int world, int64_t max_elems, void* handle_o
   c->rank = rank;
   c->world = world;
   c->max_elems = max_elems;
+  c->timeout_ticks = kTimeoutTicks;
   const int64_t bytes = area_bytes(world, max_elems);
-  hipError_t e = hipMalloc(&c->area, (size_t)bytes);
+  // uncached: the peers' xGMI stores and this rank's polling loads meet in HBM
+  hipError_t e = hipExtMallocWithFlags(&c->area, (size_t)bytes, hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->area, 0, (size_t)bytes);
   hipIpcMemHandle_t h;
   if (e == hipSuccess) e = hipIpcGetMemHandle(&h, c->area);
@@ -184,10 +216,18 @@ int vae2_syncbn_allreduce(vae2_syncbn_comm* c, double* buf, int64_t n, void* str
   a.rank = c->rank;
   a.world = c->world;
   a.max_elems = c->max_elems;
+  a.timeout_ticks = c->timeout_ticks;
   a.buf = buf;
   a.n = (int)n;
   VAE2_LAUNCH(syncbn_allreduce_kernel, dim3(1), dim3(256), 0, as_stream(stream), a);
   return check_launch(fn);
+}
+
+int vae2_syncbn_comm_set_timeout(vae2_syncbn_comm* c, double seconds) {
+  const char* fn = "vae2_syncbn_comm_set_timeout";
+  VAE2_REQUIRE(c && seconds > 0.0 && seconds <= 3600.0, fn, "bad arguments (0 < seconds <= 3600)");
+  c->timeout_ticks = (uint64_t)(seconds * kTicksPerSecond);
+  return 0;
 }
 
 int vae2_syncbn_comm_error(vae2_syncbn_comm* c, int64_t* host_out) {

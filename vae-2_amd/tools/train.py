@@ -231,6 +231,11 @@ def main(argv=None):
                 writer_dict["writer"].close()
                 logger.info("Hours: %d" % int((timeit.default_timer() - start) / 3600))
                 logger.info("Done")
+        if vdist.is_dist():
+            # the other ranks wait here for rank 0's checkpoint writes: otherwise they would
+            # start the next epoch and wait in its first SyncBN exchange, whose bounded wait
+            # can expire during a slow save
+            torch.distributed.barrier()
 
 
 if __name__ == "__main__":

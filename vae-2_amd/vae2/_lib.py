@@ -161,6 +161,7 @@ _SIGS = {
     "vae2_syncbn_comm_connect": (c_int, [c_vp, c_vp]),
     "vae2_syncbn_allreduce": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "vae2_syncbn_comm_error": (c_int, [c_vp, ctypes.POINTER(c_i64)]),
+    "vae2_syncbn_comm_set_timeout": (c_int, [c_vp, ctypes.c_double]),
     "vae2_syncbn_comm_destroy": (c_int, [c_vp]),
     "vae2_clip_normalize_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int,
                                        ctypes.POINTER(c_vp), c_vp]),
@@ -180,7 +181,7 @@ _SIGS = {
     "vae2_conv2d_set_grouping": (c_int, [c_int]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _lib = None
 
 

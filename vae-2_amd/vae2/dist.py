@@ -88,8 +88,44 @@ def all_reduce_(t, group=None):
 
 
 # ---- SyncBN statistics: one-shot IPC peer all-reduce (vae2_syncbn_allreduce) ----
-_SB = None  # (comm, group, max_elems)
 SB_MAX_ELEMS = 1 << 15  # doubles per exchange (a depth level's sums: <= 6 x 2 x 512 + 6)
+
+
+class IpcExchange:
+    """The one-shot peer all-reduce of one SyncBN group (csrc/syncbn.hip).  Every exchange
+    runs on one dedicated stream in host issue order (the same order on every rank): the
+    kernel's sequence numbers pair each exchange with the peers' same exchange even when
+    the step issues them from several streams (posterior net, past decoder)."""
+
+    def __init__(self, comm, group, max_elems):
+        self.comm, self.group, self.max_elems = comm, group, max_elems
+        self.stream = torch.cuda.Stream()
+
+    def takes(self, t, group=None):
+        return (t.is_cuda and t.dtype == torch.float64 and t.numel() <= self.max_elems and
+                t.is_contiguous() and (group is None or group is self.group or group == self.group))
+
+    def all_reduce_(self, t):
+        import ctypes
+        cur, cs = torch.cuda.current_stream(), self.stream
+        cs.wait_stream(cur)
+        call("vae2_syncbn_allreduce", self.comm, ctypes.c_void_p(t.data_ptr()), t.numel(),
+             ctypes.c_void_p(cs.cuda_stream))
+        cur.wait_stream(cs)
+
+    def error(self):
+        """Nonzero once an exchange timed out (sticky: every later exchange of this comm
+        writes NaN and exchanges nothing).  Synchronous read of the device error word."""
+        import ctypes
+        err = ctypes.c_int64(0)
+        call("vae2_syncbn_comm_error", self.comm, ctypes.byref(err))
+        return err.value
+
+    def set_timeout(self, seconds):
+        call("vae2_syncbn_comm_set_timeout", self.comm, float(seconds))
+
+
+_SB = None  # the active IpcExchange (or a test double with the same methods)
 
 
 def init_syncbn_ipc(group=None, max_elems=SB_MAX_ELEMS):
@@ -135,10 +171,7 @@ def init_syncbn_ipc(group=None, max_elems=SB_MAX_ELEMS):
         if comm.value:
             lib.vae2_syncbn_comm_destroy(comm)
         return False
-    # every exchange runs on this one stream, in host issue order (the same order on every
-    # rank): the kernel's sequence numbers pair each exchange with the peers' same exchange
-    # even when the step issues them from several streams (posterior net, past decoder)
-    _SB = (comm, g, max_elems, torch.cuda.Stream())
+    _SB = IpcExchange(comm, g, max_elems)
     return True
 
 
@@ -148,9 +181,13 @@ FORCE_IPC = False  # tests: the IPC exchange under a gloo group (ranks sharing o
 def prepare_nccl_env():
     """Environment for a NCCL (RCCL) process group whose steps are captured as HIP graphs:
     ProcessGroupNCCL's CUDA-event cache off (an event of an eager collective must never be
-    re-recorded inside a capture while the watchdog may still query it).  Call before
-    torch.distributed.init_process_group; an explicit setting wins."""
+    re-recorded inside a capture while the watchdog may still query it) and its flight
+    recorder on (vae2.graph drains the watchdog before a capture by reading which eager
+    collectives it has retired).  Call before torch.distributed.init_process_group; an
+    explicit setting wins."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    if "TORCH_NCCL_TRACE_BUFFER_SIZE" not in os.environ:
+        os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2000")
 
 
 def syncbn_exchange():
@@ -162,30 +199,28 @@ def syncbn_exchange():
 
 def syncbn_all_reduce_(t, group=None):
     """In-place sum of a SyncBN statistics buffer over the SyncBN group (float64)."""
-    if _SB is not None and t.is_cuda and t.dtype == torch.float64 and t.numel() <= _SB[2] and \
-            (group is None or group is _SB[1] or group == _SB[1]) and t.is_contiguous():
-        import ctypes
-        from ._lib import call
-        cur, cs = torch.cuda.current_stream(), _SB[3]
-        cs.wait_stream(cur)
-        call("vae2_syncbn_allreduce", _SB[0], ctypes.c_void_p(t.data_ptr()), t.numel(),
-             ctypes.c_void_p(cs.cuda_stream))
-        cur.wait_stream(cs)
+    if _SB is not None and _SB.takes(t, group):
+        _SB.all_reduce_(t)
         return
     all_reduce_(t, group=group)
 
 
+class SyncBNExchangeError(RuntimeError):
+    pass
+
+
 def syncbn_check():
-    """Raise if a SyncBN exchange timed out (a peer missing: the kernel gave up after 60 s
-    instead of hanging).  Synchronous; call at a logging point, not per step."""
+    """Raise SyncBNExchangeError if a SyncBN exchange timed out (a peer did not arrive within
+    the kernel's bound; the kernel gave up instead of hanging, wrote NaN statistics and stays
+    failed).  Synchronous; the training loop calls it at every PRINT_FREQ point and at the
+    end of each epoch (vae2/trainer.py), bench.py after its timed region."""
     if _SB is None:
         return
-    import ctypes
-    from ._lib import load
-    err = ctypes.c_int64(0)
-    load().vae2_syncbn_comm_error(_SB[0], ctypes.byref(err))
-    if err.value:
-        raise RuntimeError("SyncBN IPC exchange timed out (a rank did not arrive)")
+    if _SB.error():
+        raise SyncBNExchangeError(
+            "SyncBN IPC exchange timed out (a rank did not arrive): the batch statistics "
+            "since then are NaN on this rank and every later exchange fails; restart from "
+            "the last checkpoint")
 
 
 def bucket_allreduce(buf, bucket_elems=BUCKET_ELEMS, group=None):

@@ -394,9 +394,11 @@ def _merge(notes):
             " + ".join(n[2] for n in notes if n[2]))
 
 
-def _conv_fwd_queued(group, x, weight, bias, spec, stats):
+def _conv_fwd_queued(group, x, weight, bias, spec, stats, sp=None):
     """_conv_fwd, queued on a ConvGroup (a LazyBN input: launched at once, normalised
-    while staged)."""
+    while staged).  group None: launched at once on stream sp (a level lane, see
+    _Lanes); the output is allocated on the current stream either way."""
+    sp = stream_ptr() if sp is None else sp
     xp, xa = act_of(x)
     n, h, w, _ = x.shape
     oh, ow = spec.out_hw(h, w)
@@ -409,7 +411,11 @@ def _conv_fwd_queued(group, x, weight, bias, spec, stats):
     if lz is not None:
         call("vae2_conv2d_fwd_bnin", xp, ctypes.byref(xa), ptr(lz.save), int(lz.relu),
              ptr(packed_weight(weight, 0)), ptr(bias), yp, ctypes.byref(ya), spec.k,
-             spec.stride, spec.pad, 0.0, ptr(stats), stream_ptr())
+             spec.stride, spec.pad, 0.0, ptr(stats), sp)
+        return y
+    if group is None:
+        call("vae2_conv2d_fwd", xp, ctypes.byref(xa), ptr(packed_weight(weight, 0)), ptr(bias),
+             yp, ctypes.byref(ya), spec.k, spec.stride, spec.pad, 0.0, ptr(stats), sp)
         return y
     group.add(0, xp, xa, packed_weight(weight, 0), bias, yp, ya, spec, 0.0, stats)
     return y
@@ -522,12 +528,18 @@ class _defer_off:
         return False
 
 
-def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, group=None):
+def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, group=None,
+              sp=None, hold=None):
     """dW/db accumulated into sinks; returns (dx or None, grad for W, grad for b).  With a
     ConvGroup the data gradient is queued on it (dx is complete once it is flushed).  An
     input marked `_vae2_no_dx` (vae2.dist.anchor_reduce's output when its source needs no
-    gradient) gets none: it requires grad only to route the anchor's backward."""
-    s = stream_ptr()
+    gradient) gets none: it requires grad only to route the anchor's backward.
+    sp: launch on this stream (a level lane, _Lanes) while allocating on the current one;
+    the weight-gradient reduction then runs at once on the lane (not deferred: the deferred
+    queue is keyed by launch stream) and the workspaces go to `hold`, which the caller keeps
+    until the lane has joined."""
+    lane = sp is not None
+    s = stream_ptr() if sp is None else sp
     xp, xa = act_of(x)
     dyp, dya = act_of(dy)
     wsink, wret = _grad_sink(weight, need_w)
@@ -542,7 +554,9 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         if prof.active():
             _conv_work("wgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         lz = spec.bn_in
-        now = wret is not None or tmp_w  # not a main_grad view: reduce before returning
+        now = wret is not None or tmp_w or lane  # not a main_grad view: reduce before returning
+        if lane and hold is not None:
+            hold.append(ws)
         with _defer_off(now and _WGRAD_BATCH[0] > 0):
             if lz is not None:
                 call("vae2_conv2d_bwd_weight_bnin", xp, ctypes.byref(xa), ptr(lz.save),
@@ -574,6 +588,8 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
                 dyp, ctypes.byref(dya), ctypes.byref(dxa), spec.k, spec.stride, spec.pad)
         if rows > 0:  # + the LazyBN layer's backward partials (its reduce pass skipped)
             part = _empty((2 * rows * xa.c,), x)
+            if hold is not None:
+                hold.append(part)
             call("vae2_conv2d_bwd_data_bnpart", dyp, ctypes.byref(dya), ptr(wp), dxp,
                  ctypes.byref(dxa), spec.k, spec.stride, spec.pad, xp, ctypes.byref(xa),
                  ptr(lz.save), int(lz.relu), ptr(part), s)
@@ -737,6 +753,64 @@ def _counts_dev(counts, like):
     return t
 
 
+LEVEL_LANES = 4  # max concurrent lanes per depth level inside a graph capture (0/1: off)
+
+
+class _Lanes:
+    """The independent convolutions of one depth level on concurrent streams while a HIP
+    graph is captured (the lock-stepped HRNet branches: 18@128x256, 36@64x128, 72@32x64,
+    144@16x32 -- the same FLOPs each, but the 72 / 144-channel layers fill a quarter of the
+    chip on their own).  In the replayed graph the level is a fork/join of independent
+    kernel nodes, so the narrow layers run side by side.  Lane 0 is the current (parent)
+    stream; lane k > 0 a stream of its own per (parent, k), forked from the parent before
+    the level and joined into it after.  Every buffer is allocated on the parent stream and
+    kept alive until the join (callers hold them), so the allocator never sees lane uses.
+    Layers whose data gradients accumulate into one buffer (a shared GradLink) share a lane.
+    Eager steps and profiled steps keep one stream (a stream switch costs host time there)."""
+
+    def __init__(self, specs):
+        self.on = (LEVEL_LANES > 1 and len(specs) > 1 and torch.cuda.is_available() and
+                   not prof.active() and torch.cuda.is_current_stream_capturing())
+        self.lane = [0] * len(specs)
+        if not self.on:
+            return
+        keys = []
+        for i, sp in enumerate(specs):
+            key = id(sp.x_link) if sp.x_link is not None else ("solo", i)
+            if key not in keys:
+                keys.append(key)
+            self.lane[i] = keys.index(key) % LEVEL_LANES
+        if max(self.lane) == 0:
+            self.on = False
+            return
+        self.parent = torch.cuda.current_stream()
+        self.streams = {}
+        for k in sorted(set(self.lane) - {0}):
+            st = streams.side_stream(self.parent.device, ("lane", self.parent.cuda_stream, k))
+            st.wait_stream(self.parent)
+            streams._FORKED.add(st)
+            self.streams[k] = st
+
+    def ptr(self, i):
+        """Launch stream of layer i (None: the current stream)."""
+        if not self.on or self.lane[i] == 0:
+            return None
+        return ctypes.c_void_p(self.streams[self.lane[i]].cuda_stream)
+
+    def join(self):
+        if self.on:
+            for st in self.streams.values():
+                self.parent.wait_stream(st)
+
+    def sync(self):
+        """Join, then fork again: parent work issued now is ordered with every lane's work
+        before and after it."""
+        if self.on:
+            self.join()
+            for st in self.streams.values():
+                st.wait_stream(self.parent)
+
+
 class _ConvBNMulti(torch.autograd.Function):
     """n independent conv -> BatchNorm(train) [-> +residual] [-> ReLU] layers (one HRNet
     depth level): the convs launch per layer, every BatchNorm step is one launch for all
@@ -752,8 +826,9 @@ class _ConvBNMulti(torch.autograd.Function):
         L = [flat[6 * i:6 * i + 6] for i in range(n)]
         group = _bn_group()
         rs, saves, fins, counts, cs = [], [], [], [], []
-        cg = ConvGroup()
-        for (x, weight, bias, gamma, beta, residual), spec in zip(L, specs):
+        lanes = _Lanes(specs)
+        cg = None if lanes.on else ConvGroup()
+        for li, ((x, weight, bias, gamma, beta, residual), spec) in enumerate(zip(L, specs)):
             nn_, h, w, _ = x.shape
             oh, ow = spec.out_hw(h, w)
             cout = weight.shape[0]
@@ -762,12 +837,14 @@ class _ConvBNMulti(torch.autograd.Function):
                                                   ctypes.byref(Act(nn_, oh, ow, cout, cout)),
                                                   spec.k, spec.stride, spec.pad)
             stats = _empty((2 * rows * cout,), x)
-            rs.append(_conv_fwd_queued(cg, x, weight, bias, spec, stats))
+            rs.append(_conv_fwd_queued(cg, x, weight, bias, spec, stats, lanes.ptr(li)))
             saves.append(_empty((4 * cout,), x))
             counts.append(float(nn_ * oh * ow))
             cs.append(cout)
             fins.append((stats, rows))
-        cg.flush()  # the level's convs: direct-3x3 layers share launches
+        if cg is not None:
+            cg.flush()  # the level's convs: direct-3x3 layers share launches
+        lanes.join()
         tot = 2 * sum(cs)
         buf = _empty((tot + n,), rs[0], torch.float64)
         world = 1
@@ -958,7 +1035,11 @@ class _ConvBNMulti(torch.autograd.Function):
         call("vae2_bn_multi_bwd_apply", len(act), (_lib.BnLayer * len(act))(*[lay[i] for i in act]),
              s)
         grads = [None]
-        cg = ConvGroup()  # the level's data gradients: direct-3x3 layers share launches
+        lanes = _Lanes(specs)
+        # the level's data gradients: direct-3x3 layers share launches (one stream), or the
+        # layers run on concurrent lanes (graph capture)
+        cg = None if lanes.on else ConvGroup()
+        hold = []
         with wgrad_batch():  # the level's weight-gradient reductions in one launch
             for i in range(n):
                 spec = specs[i]
@@ -970,15 +1051,20 @@ class _ConvBNMulti(torch.autograd.Function):
                     if link.buf is None:
                         link.buf = dres
                     elif link.buf is not dres:  # (dres is link.buf: summed in the BN kernel)
-                        if cg.pending(link.buf):
+                        if cg is not None and cg.pending(link.buf):
                             cg.flush()
+                        if lanes.on:  # a lane may still be writing it
+                            lanes.sync()
                         link.buf.add_(dres)
                     dres = link.finish()
                 dx, wret, bret_conv = _conv_bwd(x, weight, bias, drs[i], spec, need[1 + 6 * i],
                                                 need[1 + 6 * i + 1], need[1 + 6 * i + 2],
-                                                group=cg)
+                                                group=cg, sp=lanes.ptr(i), hold=hold)
                 grads += [dx, wret, bret_conv, gret, bret, dres]
-            cg.flush()
+            if cg is not None:
+                cg.flush()
+            lanes.join()
+        del hold  # (after the join: the lanes' workspaces return to the parent's pool)
         return tuple(grads)
 
 

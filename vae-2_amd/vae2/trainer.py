@@ -149,8 +149,10 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
         else:
             reduced_loss_D = torch.zeros(1)
             loss_D_sequence = loss_D_frame = 0.0
-        if getattr(fm, "defer_checks", False) and i_iter % config.PRINT_FREQ == 0:
-            fm.check_anomalies()  # deferred NaN/Inf flag (utils.py:63-65), one sync
+        if i_iter % config.PRINT_FREQ == 0:
+            if getattr(fm, "defer_checks", False):
+                fm.check_anomalies()  # deferred NaN/Inf flag (utils.py:63-65), one sync
+            vdist.syncbn_check()  # a timed-out IPC SyncBN exchange raises here
         batch_time.update(time.time() - tic)
         tic = time.time()
         ave_loss_D.update(float(reduced_loss_D.item()))
@@ -180,3 +182,4 @@ def adversarial_train(config, epoch, num_epoch, epoch_iters, base_lr, num_iters,
                              ("train_loss_x2t_gan_frame", f(loss_x2t_gan_frame))):
                 writer.add_scalar(tag, val, global_steps)
             writer_dict["train_global_steps"] = global_steps + 1
+    vdist.syncbn_check()  # once per epoch as well (the last iterations after a PRINT_FREQ point)
