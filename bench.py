@@ -100,7 +100,7 @@ def parse():
                          "discriminators) + the discriminator step with its own Adam")
     ap.add_argument("--level-lanes", type=int, default=None,
                     help="concurrent streams per HRNet depth level inside the captured graph "
-                         "(vae2.ops.LEVEL_LANES; 0/1: one stream)")
+                         "(vae2.ops.LEVEL_LANES; 0/1: one stream; negative: forward only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto = on, at every world "
                          "size: the distributed step's RCCL collectives are captured in "
@@ -270,7 +270,8 @@ def main():
             raise SystemExit(f"conv tune key {k}: unknown key or out-of-range value {v}")
     if args.level_lanes is not None:
         from vae2 import ops as vops
-        vops.LEVEL_LANES = args.level_lanes
+        vops.LEVEL_LANES = abs(args.level_lanes)
+        vops.LEVEL_LANES_BWD = args.level_lanes > 0  # negative: forward only
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False

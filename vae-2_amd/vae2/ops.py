@@ -753,7 +753,8 @@ def _counts_dev(counts, like):
     return t
 
 
-LEVEL_LANES = 4  # max concurrent lanes per depth level inside a graph capture (0/1: off)
+LEVEL_LANES = 0  # concurrent lanes per depth level inside a graph capture (0/1: off; measured slower)
+LEVEL_LANES_BWD = True  # lanes in the backward as well
 
 
 class _Lanes:
@@ -768,11 +769,11 @@ class _Lanes:
     Layers whose data gradients accumulate into one buffer (a shared GradLink) share a lane.
     Eager steps and profiled steps keep one stream (a stream switch costs host time there)."""
 
-    def __init__(self, specs):
-        self.on = (LEVEL_LANES > 1 and len(specs) > 1 and torch.cuda.is_available() and
-                   not prof.active() and torch.cuda.is_current_stream_capturing())
+    def __init__(self, specs, enabled=True):
+        self.on = False
         self.lane = [0] * len(specs)
-        if not self.on:
+        if (not enabled or LEVEL_LANES <= 1 or len(specs) < 2 or not torch.cuda.is_available()
+                or prof.active()):
             return
         keys = []
         for i, sp in enumerate(specs):
@@ -781,15 +782,24 @@ class _Lanes:
                 keys.append(key)
             self.lane[i] = keys.index(key) % LEVEL_LANES
         if max(self.lane) == 0:
-            self.on = False
             return
         self.parent = torch.cuda.current_stream()
-        self.streams = {}
-        for k in sorted(set(self.lane) - {0}):
-            st = streams.side_stream(self.parent.device, ("lane", self.parent.cuda_stream, k))
+        # only the main (capture) stream forks lanes: a second-level fork -- lanes forked
+        # from a side stream that is itself forked from the capture stream (the posterior
+        # net's, the past decoder's) -- makes HIP's stream-capture end segfault (ROCm 7.0
+        # runtime; reproduced with plain torch ops by scripts/probe_lane_capture.py, nest
+        # mode); those sub-networks already run beside the main stream's work
+        if streams.role_of(self.parent) != "main":
+            return
+        # the lane streams exist before the capture (created by the eager warm-up steps)
+        self.streams = {k: streams.side_stream(self.parent.device, ("lane", "main", k))
+                        for k in sorted(set(self.lane) - {0})}
+        self.on = torch.cuda.is_current_stream_capturing()
+        if not self.on:
+            return
+        for st in self.streams.values():
             st.wait_stream(self.parent)
             streams._FORKED.add(st)
-            self.streams[k] = st
 
     def ptr(self, i):
         """Launch stream of layer i (None: the current stream)."""
@@ -1035,7 +1045,7 @@ class _ConvBNMulti(torch.autograd.Function):
         call("vae2_bn_multi_bwd_apply", len(act), (_lib.BnLayer * len(act))(*[lay[i] for i in act]),
              s)
         grads = [None]
-        lanes = _Lanes(specs)
+        lanes = _Lanes(specs, LEVEL_LANES_BWD)
         # the level's data gradients: direct-3x3 layers share launches (one stream), or the
         # layers run on concurrent lanes (graph capture)
         cg = None if lanes.on else ConvGroup()

@@ -28,6 +28,15 @@ def side_stream(device, idx):
     return s
 
 
+def role_of(stream):
+    """The side-stream key of `stream`, or "main" (the default, a graph's capture stream or
+    any other stream the caller runs on)."""
+    for key, s in _SIDE.items():
+        if s == stream:
+            return key[1]
+    return "main"
+
+
 def _record(tensors, stream):
     for t in tensors:
         if isinstance(t, (list, tuple)):
