@@ -15,11 +15,18 @@
 namespace vae2 {
 
 // ---------------------------------------------------- partial reductions ----
-// Pixels per block for per-channel reductions.
-static int64_t pix_per_block(int64_t P) {
-  int64_t ppb = ceil_div(P, 1024);
-  if (ppb < 32) ppb = 32;
-  return ppb;
+// Pixels per block for per-channel reductions: whole passes of the quad-path block
+// (quad_rows(C) pixel rows x kApplyU pixels per thread), as many passes as keep the layer
+// at <= 1024 blocks.  (Round 5 took ceil(P / 1024), at least 32, for every C: the narrow
+// layers' blocks then ran one partial pass -- a 36-channel block covered 64 of the 112
+// pixels its threads load, a 72-channel one 32 of 56 -- and the 18 / 36 / 72 backward
+// reduce launches streamed at 0.34 of the HBM peak.)
+static inline int quad_rows(int64_t C);
+constexpr int kPassU = 4;  // = kApplyU (defined with the apply kernels below)
+static int64_t pix_per_block(int64_t P, int64_t C) {
+  const int64_t pass = (int64_t)quad_rows(C) * kPassU;
+  const int64_t n = ceil_div(P, 1024 * pass);
+  return pass * (n > 0 ? n : 1);
 }
 
 // Mode 0: (sum x, sum x^2).  Mode 1: BN backward (sum g, sum g*xhat).
@@ -123,8 +130,11 @@ __device__ __forceinline__ void st4(float* p, f4 v, int c, int C) {
   }
 }
 
-static inline int quad_rows(int64_t C) { return 256 / (int)((C + 3) / 4); }
-constexpr int kApplyU = 4;  // pixels per thread in the apply kernels (2: 852 vs 861, 8: 841 vs 853 frames/s, round-4 A/B)
+static inline int quad_rows(int64_t C) {
+  const int c4 = (int)((C + 3) / 4);
+  return c4 <= 256 ? 256 / c4 : 1;
+}
+constexpr int kApplyU = kPassU;  // pixels per thread in the apply kernels (2: 852 vs 861, 8: 841 vs 853 frames/s, round-4 A/B)
 
 __global__ __launch_bounds__(256) void bn_apply_q_kernel(
     const float* __restrict__ x, Act xd, const float* __restrict__ save,
@@ -1352,7 +1362,7 @@ extern "C" {
 
 int64_t vae2_bn_partial_rows(const vae2_act* xd) {
   int64_t P = act_pixels(xd);
-  return ceil_div(P, pix_per_block(P));
+  return ceil_div(P, pix_per_block(P, xd->c));
 }
 
 int vae2_bn_stats(const float* x, const vae2_act* xd, float* partials,
@@ -1360,7 +1370,7 @@ int vae2_bn_stats(const float* x, const vae2_act* xd, float* partials,
   const char* fn = "vae2_bn_stats";
   VAE2_REQUIRE(x && partials && act_ok(xd), fn, "bad arguments");
   int64_t P = act_pixels(xd);
-  int64_t ppb = pix_per_block(P);
+  int64_t ppb = pix_per_block(P, xd->c);
   Act a = to_act(xd);
   if (quad_ok(xd->c) && v4_ok(x, xd->ps)) {
     VAE2_LAUNCH((chan_partials_q_kernel<0>), dim3((unsigned)ceil_div(P, ppb)), dim3(256),
@@ -1511,7 +1521,7 @@ int vae2_bn_relu_bwd_reduce(const float* dy, const vae2_act* dyd,
   VAE2_REQUIRE(dy && x && save && partials && act_ok(dyd) && act_ok(xd), fn, "bad arguments");
   VAE2_REQUIRE(!y || act_ok(yd), fn, "bad y descriptor");
   int64_t P = act_pixels(xd);
-  int64_t ppb = pix_per_block(P);
+  int64_t ppb = pix_per_block(P, xd->c);
   Act ya = (relu && y) ? to_act(yd) : to_act(xd);
   if (!relu) y = nullptr;
   if (quad_ok(xd->c) && v4_ok(x, xd->ps) && v4_ok(dy, dyd->ps) && (!y || v4_ok(y, yd->ps))) {
@@ -1629,7 +1639,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       L.rows = quad_rows(l.xd.c);
       L.blk0 = blocks;
       if (kind == 1) {
-        L.ppb = pix_per_block(L.P);
+        L.ppb = pix_per_block(L.P, L.C);
         blocks += (int)ceil_div(L.P, L.ppb);
       } else {
         blocks += (int)ceil_div(L.P, (int64_t)L.rows * kApplyU);
