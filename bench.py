@@ -37,6 +37,7 @@ Printed JSON also carries:
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -101,6 +102,9 @@ def parse():
     ap.add_argument("--level-lanes", type=int, default=None,
                     help="concurrent streams per HRNet depth level inside the captured graph "
                          "(vae2.ops.LEVEL_LANES; 0/1: one stream; negative: forward only)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 passes over the dominant kernel (PMC HBM "
+                         "traffic, trace-averaged duration)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (auto = on, at every world "
                          "size: the distributed step's RCCL collectives are captured in "
@@ -142,6 +146,84 @@ def build_models(config, with_d=False):
         return ed, ez
     return (ed, ez, models.enc_hrnet.get_D_sequence_model(config),
             models.enc_hrnet.get_D_frame_model(config))
+
+
+def _child_args(args):
+    """bench.py arguments of a child run with this run's workload and kernel choices."""
+    a = ["--cfg", args.cfg, "--dtype", args.dtype, "--lazy-bn", args.lazy_bn,
+         "--side-streams", args.side_streams, "--conv-grouping", args.conv_grouping]
+    for flag, v in (("--batch", args.batch), ("--height", args.height), ("--width", args.width),
+                    ("--clip-length", args.clip_length), ("--conv-algo", args.conv_algo),
+                    ("--heads-algo", args.heads_algo), ("--level-lanes", args.level_lanes)):
+        if v is not None:
+            a += [flag, str(v)]
+    if args.conv_tune:
+        a += ["--conv-tune", args.conv_tune]
+    if args.full_step:
+        a += ["--full-step"]
+    return a
+
+
+def _kname(name):
+    return re.sub(r"\(.*\)$", "", name).replace("vae2::", "").replace("void ", "").strip()
+
+
+def live_kernel_passes(args, kernel):
+    """rocprofv3 over child runs of this benchmark, restricted to the dominant kernel
+    (MI355X_MICROARCH.md HBM / rocprofv3 recipe): one --pmc FETCH_SIZE pass and one --pmc
+    WRITE_SIZE pass over 2 eager steps (separate passes, the counters' own runs), and one
+    --kernel-trace --stats pass over 3 graph-replayed steps (the timed region's form).
+    Returns ({hbm bytes per launch, fetch/write split, launches}, {trace avg us, calls}) or
+    Nones with the reason -- measured in this run, not looked up."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(ROOT, "vae-2_amd", "tools"))
+    import pmc_traffic as pt
+    regex = re.sub(r"[<>()\[\]*+?.|^$]", ".", kernel)
+    base = [sys.executable, os.path.abspath(__file__), "--warmup", "1", "--no-cpu-baseline",
+            "--no-roofline", "--no-pmc"] + _child_args(args)
+    env = dict(os.environ, TMPDIR="/tmp")
+    tmp = tempfile.mkdtemp(prefix="vae2_rocprof_", dir="/tmp")
+    try:
+        def run(extra, sub, tail):
+            cmd = [exe] + extra + ["--kernel-include-regex", regex, "-f", "csv", "-d",
+                                   os.path.join(tmp, sub), "-o", "run", "--"] + base + tail
+            r = subprocess.run(cmd, timeout=300, capture_output=True, env=env, cwd=ROOT)
+            return r.returncode
+        vals = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            rc = run(["--pmc", c], c, ["--steps", "2", "--graph", "off"])
+            if rc != 0:
+                return None, None, f"rocprofv3 --pmc {c} pass exited {rc}"
+            vals[c] = pt.per_launch(os.path.join(tmp, c), c, kernel)
+            if not vals[c]:
+                return None, None, f"no {c} samples for {kernel}"
+        fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 1024 * 2.0
+        write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
+        pmc = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch,
+               "write_bytes_per_launch": write, "launches": len(vals["FETCH_SIZE"]),
+               "note": "FETCH_SIZE x2 (gfx950 16-byte-read calibration) + WRITE_SIZE, KiB x1024, "
+                       "mean over the dominant kernel's launches of 2 eager steps"}
+        trace = None
+        if run(["--kernel-trace", "--stats"], "trace", ["--steps", "3", "--graph", "on"]) == 0:
+            import csv
+            import glob
+            for f in glob.glob(os.path.join(tmp, "trace", "**", "*kernel_stats.csv"),
+                               recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if _kname(row["Name"]) == kernel:
+                            trace = {"avg_us": float(row["AverageNs"]) / 1e3,
+                                     "calls": int(row["Calls"])}
+        return pmc, trace, None
+    except subprocess.TimeoutExpired as e:
+        return None, None, f"rocprofv3 pass timed out ({e.timeout} s)"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def pmc_traffic(kernel):
@@ -405,9 +487,30 @@ def main():
             conv_gf = sum(r.get("gflop_per_step", 0.0) for r in summ["families"])
             ref_gf = REF_GFLOP_PER_CLIP.get((H, W))
             roof = dict(dom)
-            tr = pmc_traffic(dom["kernel"])
-            roof["traffic"] = round(tr["hbm_bytes_per_launch"]) if tr else None
-            roof["traffic_unit"] = "HBM bytes/launch (PMC, profiles/)"
+            live, trace, why = (None, None, "--no-pmc") if args.no_pmc or world > 1 else \
+                live_kernel_passes(args, dom["kernel"])
+            if live is not None:
+                roof["traffic"] = round(live["hbm_bytes_per_launch"])
+                roof["traffic_unit"] = "HBM bytes/launch (PMC, measured in this run)"
+                roof["traffic_detail"] = {k: (round(v) if isinstance(v, float) else v)
+                                          for k, v in live.items()}
+                if roof.get("algorithmic_bytes_per_launch"):
+                    roof["traffic_over_algorithmic"] = round(
+                        live["hbm_bytes_per_launch"] / roof["algorithmic_bytes_per_launch"], 3)
+            else:  # fall back to the newest committed measurement of the same kernel
+                tr = pmc_traffic(dom["kernel"])
+                roof["traffic"] = round(tr["hbm_bytes_per_launch"]) if tr else None
+                roof["traffic_unit"] = (f"HBM bytes/launch (PMC, committed profiles/; live "
+                                        f"pass unavailable: {why})")
+            if trace is not None:
+                # the same kernel in the timed region's form (graph replay, side streams
+                # concurrent) from rocprofv3's kernel trace: achieved over the trace average
+                t_us = trace["avg_us"]
+                roof["trace"] = {"avg_us": round(t_us, 2), "calls": trace["calls"],
+                                 "achieved": round(roof["achieved"] * roof["avg_launch_us"] / t_us, 2),
+                                 "frac": round(roof["frac"] * roof["avg_launch_us"] / t_us, 4),
+                                 "source": "rocprofv3 --kernel-trace --stats, 3 graph-replayed "
+                                           "steps of this workload, this run"}
             roof["step_frac"] = round(conv_gf / ms / prof.MFMA_PEAK_TF, 4)
             roof["step_gflop"] = round(conv_gf, 1)
             if ref_gf is not None and L == 3 and not full:

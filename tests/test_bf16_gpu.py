@@ -246,13 +246,18 @@ def _with_bf16(on, fn):
 def test_bf16_per_module_gradients(stage):
     """Per-module bf16 check: the first HighResolutionModule of an HRNet
     stage (lock-stepped BasicBlock branches + fuse rows, training BatchNorm) run once with
-    fp32 and once with bf16 MFMA operands on IDENTICAL fp32 inputs and upstream gradients:
-    median cosine >= 0.995 and every parameter / input gradient cosine >= 0.98 with its
-    norm within 5 % of the fp32-operand one, outputs within 2e-2.  Inside one module the
-    chaos of the whole network (tests/diag_grad_chaos.py) does not build up; the lowest
-    cosines are BatchNorm bias gradients (a per-channel sum over all pixels of a gradient
-    that largely cancels: bf16 rounding of every conv operand shows most there; measured
-    stage 2 min 0.994, stage 3 0.981, stage 4 0.982; heads 0.9988)."""
+    fp32 and once with bf16 MFMA operands on IDENTICAL fp32 inputs and upstream gradients.
+
+    The bar is calibrated in the test, not fitted to the bf16 result: a
+    third run keeps fp32 operands but rounds only the module's conv WEIGHTS to bf16 once --
+    the sensitivity of each gradient to one bf16 rounding of one operand.  The bf16-operand
+    path rounds three operands of every conv product (forward: activation and weight; data
+    gradient: gradient and weight; weight gradient: activation and gradient), so per tensor
+    1 - cos(bf16, fp32) <= 3 x (1 - cos(weights-rounded, fp32)) + 1e-3 (an absolute floor
+    for tensors the weight rounding barely moves), every norm within 5 % and outputs within
+    2e-2.  Inside one module the chaos of the whole network (tests/diag_grad_chaos.py) does
+    not build up; the most sensitive tensors are BatchNorm bias gradients (per-channel sums
+    of a largely cancelling gradient), and the calibration run shows that sensitivity too."""
     from helpers import build, make_cfg
     from vae2 import ops
     ed, _ = build(make_cfg(arch="w18", hw=(64, 128)))
@@ -270,9 +275,14 @@ def test_bf16_per_module_gradients(stage):
     shapes = [(2, 64 >> i, 128 >> i, c) for i, c in enumerate(chans)]
     xs_cpu = [torch.randn(s, generator=g) for s in shapes]
 
-    def run(on):
+    def run(on, round_weights=False):
         import copy
         mod = copy.deepcopy(mod0).to(DEV)
+        if round_weights:
+            with torch.no_grad():
+                for m in mod.modules():
+                    if isinstance(m, torch.nn.Conv2d):
+                        m.weight.copy_(m.weight.to(torch.bfloat16).float())
         xs = []
         for x in xs_cpu:
             t_ = ops.new_act(x.shape, torch.empty(1, device=DEV))
@@ -293,32 +303,43 @@ def test_bf16_per_module_gradients(stage):
 
     y32, gx32, gp32 = run(False)
     y16, gx16, gp16 = run(True)
+    _, gxw, gpw = run(False, round_weights=True)
     for a, b in zip(y16, y32):
         assert rel(a, b) < 2e-2
-    rows = [(f"x{i}", _cos(a, b), float(a.norm() / b.norm())) for i, (a, b) in enumerate(zip(gx16, gx32))]
-    rows += [(n, _cos(gp16[n], gp32[n]), float(gp16[n].norm() / (gp32[n].norm() + 1e-30)))
+    rows = [(f"x{i}", _cos(a, b), float(a.norm() / b.norm()), _cos(w, b))
+            for i, (a, b, w) in enumerate(zip(gx16, gx32, gxw))]
+    rows += [(n, _cos(gp16[n], gp32[n]), float(gp16[n].norm() / (gp32[n].norm() + 1e-30)),
+              _cos(gpw[n], gp32[n]))
              for n in gp32 if float(gp32[n].norm()) > 0]
     worst = min(rows, key=lambda r: r[1])
-    print(f"{stage}: {len(rows)} gradients, min cosine {worst[1]:.5f} ({worst[0]}), "
-          f"norm ratios {min(r[2] for r in rows):.4f} .. {max(r[2] for r in rows):.4f}")
-    bad = [r for r in rows if r[1] < 0.98 or abs(r[2] - 1) > 0.05]
+    print(f"{stage}: {len(rows)} gradients, min cosine {worst[1]:.5f} ({worst[0]}; "
+          f"weights-rounded calibration {worst[3]:.5f}), norm ratios "
+          f"{min(r[2] for r in rows):.4f} .. {max(r[2] for r in rows):.4f}, max (1-cos) / "
+          f"calibration {max((1 - r[1]) / max(1 - r[3], 1e-9) for r in rows):.2f}")
+    bad = [r for r in rows if (1 - r[1]) > 3 * (1 - r[3]) + 1e-3 or abs(r[2] - 1) > 0.05]
     assert not bad, bad
-    assert sorted(r[1] for r in rows)[len(rows) // 2] >= 0.995
 
 
 def test_bf16_heads_gradients():
     """The three 270-channel heads (per-branch 1x1 products, up-sum, BN, output conv) with
-    fp32 vs bf16 MFMA operands on identical inputs and upstream gradient: every parameter
-    and input gradient cosine >= 0.99, norm within 5 %."""
+    fp32 vs bf16 MFMA operands on identical inputs and upstream gradient, held to the
+    in-test calibration of test_bf16_per_module_gradients (1 - cos <= 3 x that of a run
+    with only the conv weights rounded to bf16, + 1e-3), every norm within 5 %."""
     import copy
     from test_heads_gpu import _heads_and_inputs
     from vae2 import heads as vheads
     heads, ys = _heads_and_inputs("w18", (64, 128), 2, seed=23)
     gout = None
 
-    def run(on):
+    def run(on, round_weights=False):
         nonlocal gout
         hh = [copy.deepcopy(h).to(DEV) for h in heads]
+        if round_weights:
+            with torch.no_grad():
+                for h in hh:
+                    for m in h.modules():
+                        if isinstance(m, torch.nn.Conv2d):
+                            m.weight.copy_(m.weight.to(torch.bfloat16).float())
         yh = [y.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_() for y in ys]
 
         def step():
@@ -339,8 +360,11 @@ def test_bf16_heads_gradients():
 
     g32 = run(False)
     g16 = run(True)
-    rows = [(n, _cos(g16[n], g32[n]), float(g16[n].norm() / (g32[n].norm() + 1e-30)))
+    gw = run(False, round_weights=True)
+    rows = [(n, _cos(g16[n], g32[n]), float(g16[n].norm() / (g32[n].norm() + 1e-30)),
+             _cos(gw[n], g32[n]))
             for n in g32 if float(g32[n].norm()) > 0]
-    print(f"heads: {len(rows)} gradients, min cosine {min(r[1] for r in rows):.5f}")
-    bad = [r for r in rows if r[1] < 0.99 or abs(r[2] - 1) > 0.05]
+    print(f"heads: {len(rows)} gradients, min cosine {min(r[1] for r in rows):.5f}, max "
+          f"(1-cos) / calibration {max((1 - r[1]) / max(1 - r[3], 1e-9) for r in rows):.2f}")
+    bad = [r for r in rows if (1 - r[1]) > 3 * (1 - r[3]) + 1e-3 or abs(r[2] - 1) > 0.05]
     assert not bad, bad
