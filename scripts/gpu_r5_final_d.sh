@@ -3,7 +3,7 @@
 # then the PMC HBM traffic of the kernel the default line reports as dominant.
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r5i}
-bash scripts/gpu_r5_final_a.sh $TAG || exit 1
+bash scripts/archive/gpu_r5_final_a.sh $TAG || exit 1
 K=$(grep '^{' gpurun_out/${TAG}_bench_default.log | python -c 'import json,sys; print(json.loads(sys.stdin.read())["roofline"]["kernel"])')
 echo "dominant: $K"
 bash scripts/gpu_pmc.sh ${TAG}_dom "$K" || exit 1

@@ -1,4 +1,4 @@
-"""Reduce rocprofv3 --pmc counter CSVs (scripts/gpu_narrow_pmc.sh passes) to one JSON:
+"""Reduce rocprofv3 --pmc counter CSVs (scripts/archive/gpu_narrow_pmc.sh passes) to one JSON:
 per kernel instance, the mean of each counter over its dispatches, plus derived ratios
 (wait / active shares of wave cycles, VALU and LDS instructions per MFMA, MFMA busy share).
 
