@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--lazy-bn", choices=("on", "off"), default="on",
                     help="BasicBlock bn1 normalised inside conv2's staging, never stored "
                          "(vae2.ops.LazyBN; A/B)")
+    ap.add_argument("--part-bn", choices=("on", "off"), default="on",
+                    help="BatchNorm backward partials from the single consumer conv's data-"
+                         "gradient epilogue where that conv is a 1x1 GEMM / gather-kernel conv "
+                         "(vae2.ops.PartBN; A/B)")
     ap.add_argument("--conv-algo", type=int, default=None,
                     help="vae2_conv2d_set_algo bits (A/B of kernel choices; default: auto)")
     ap.add_argument("--heads-algo", type=int, default=None,
@@ -151,6 +155,7 @@ def build_models(config, with_d=False):
 def _child_args(args):
     """bench.py arguments of a child run with this run's workload and kernel choices."""
     a = ["--cfg", args.cfg, "--dtype", args.dtype, "--lazy-bn", args.lazy_bn,
+         "--part-bn", args.part_bn,
          "--side-streams", args.side_streams, "--conv-grouping", args.conv_grouping]
     for flag, v in (("--batch", args.batch), ("--height", args.height), ("--width", args.width),
                     ("--clip-length", args.clip_length), ("--conv-algo", args.conv_algo),
@@ -357,6 +362,9 @@ def main():
     if args.lazy_bn == "off":
         from vae2 import ops as vops
         vops.LAZY_BN = False
+    if args.part_bn == "off":
+        from vae2 import ops as vops
+        vops.PART_BN = False
     if args.dtype == "bf16":
         from vae2 import _lib
         _lib.load().vae2_conv2d_set_mfma_bf16(1)

@@ -164,7 +164,11 @@ int vae2_conv2d_fwd(const float* x, const vae2_act* xd, const float* wp,
  * also produce the BatchNorm layer's backward partials [2][rows][C] (sum g, sum g*xhat
  * with g the incoming gradient masked by the ReLU, as vae2_bn_relu_bwd_reduce writes)
  * in the epilogue: rows = vae2_conv2d_bwd_data_bnpart_rows (0 = not available for
- * this geometry); bn_x = the BatchNorm's pre-BN input (shape of dx).               */
+ * this geometry); bn_x = the BatchNorm's pre-BN input (shape of dx).  Since round 6
+ * (same ABI) every data-gradient kernel family writes them -- the direct 3x3 kernels,
+ * the persistent 1x1 GEMM and the gather kernel (1x1, 3x3, stride-2 parity classes) --
+ * so any conv that is the ONLY consumer of a stored BatchNorm(+ReLU) output without
+ * residual can replace that layer's backward reduce pass (vae2/ops.py PartBN).      */
 int vae2_conv2d_bnin_ok(const float* x, const vae2_act* xd, const vae2_act* yd, int k,
                         int stride, int pad);
 int vae2_conv2d_fwd_bnin(const float* x, const vae2_act* xd, const float* bn_save, int relu,

@@ -120,6 +120,15 @@ struct IGemm {
   int vec_out;   // y 16-byte aligned, y_ps % 4 == 0, no statistics with beta != 0
   FastDiv hw_div, w_div;  // divide by g_h*g_w, g_w
   int ktab;               // use the K-step table (set_tune key 12, default on)
+  // Data gradient (ROLE 1) with bx set (round 6): y is the gradient of a BatchNorm(+ReLU)
+  // layer's output whose only consumer is this conv; the epilogue writes that layer's
+  // backward partials (sum g, sum g*xhat; g = y masked by the ReLU recomputed from bx)
+  // into stats, [2][gridDim.x * gridDim.z][n] (row = class * gridDim.x + tile), instead of
+  // the layer's own reduce pass.  bx = its pre-BN tensor (y's pixels and channels).
+  const float* bx;
+  int bx_ps, brelu;
+  const float* bsave;
+  uint32_t bx_bytes;
   // Strided data gradient: one launch covers every stride-parity class of the input
   // pixels, class = blockIdx.z (gridDim.z == 1: the fields above are used as they are).
   struct Cls {
@@ -394,6 +403,29 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  // producer BatchNorm backward partials (data gradient, bx set): per-column mean, invstd,
+  // scale, shift of that layer (bn_bwd_reduce_body's arithmetic, element by element)
+  constexpr bool BP = ROLE == 1 && !BF;
+  const bool bnp = BP && p.bx != nullptr;
+  float bmn[BP ? TN : 1], bis[BP ? TN : 1], bsc[BP ? TN : 1], bsh[BP ? TN : 1];
+  if constexpr (BP) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + j * 16 + r < p.n ? n0 + j * 16 + r : p.n - 1;
+      bmn[j] = bnp ? p.bsave[n] : 0.f;
+      bis[j] = bnp ? p.bsave[p.n + n] : 0.f;
+      bsc[j] = bnp ? p.bsave[2 * p.n + n] : 0.f;
+      bsh[j] = bnp ? p.bsave[3 * p.n + n] : 0.f;
+    }
+  }
+  // output pixel of GEMM row m (m < M)
+  auto pix_of = [&](int m) {
+    const int gn = (int)p.hw_div.div((uint32_t)m);
+    const int rem = m - gn * p.g_h * p.g_w;
+    const int gi = (int)p.w_div.div((uint32_t)rem);
+    const int gj = rem - gi * p.g_w;
+    return (gn * p.y_h + gi * p.y_step + p.y_offh) * p.y_w + gj * p.y_step + p.y_offw;
+  };
   if (p.vec_out && (KS == 1 || wave == 0)) {
     // statistics in the MFMA layout (beta = 0 whenever they are requested), then each
     // 16x16 tile transposed inside lane quads: one 16-byte store per lane and tile, and
@@ -401,7 +433,36 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
     const int k = r & 3, qc = 4 * (r >> 2);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      if (p.stats) {
+      if (BP && bnp && p.stats) {
+        // the row tile's 4 x TN pre-BN values, one batch of range-checked loads
+        const __amdgpu_buffer_rsrc_t bxr = make_rsrc(p.bx, p.bx_bytes);
+        float xv[4][TN];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int me = mw + i * 16 + g * 4 + e;
+          const bool mok = me < M;
+          const int pix = pix_of(mok ? me : 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            xv[e][j] = load1(bxr, mok && n < p.n ? (uint32_t)(pix * p.bx_ps + n) * 4u : kOOB);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool mok = mw + i * 16 + g * 4 + e < M;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            const float v = acc[i][j][e];
+            const float x = xv[e][j];
+            const float gv = (p.brelu && !(__builtin_fmaf(x, bsc[j], bsh[j]) > 0.f)) ? 0.f : v;
+            const bool ok = mok && n < p.n;
+            csum[j] += ok ? gv : 0.f;
+            csq[j] += ok ? gv * (x - bmn[j]) * bis[j] : 0.f;
+          }
+        }
+      } else if (p.stats) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (mw + i * 16 + g * 4 + e >= M) continue;
@@ -469,6 +530,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       const int oy = gi * p.y_step + p.y_offh;
       const int ox = gj * p.y_step + p.y_offw;
       float* yrow = p.y + ((gn * p.y_h + oy) * p.y_w + ox) * p.y_ps;
+      const float* xrow = BP && bnp ? p.bx + ((gn * p.y_h + oy) * p.y_w + ox) * p.bx_ps : nullptr;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + j * 16 + r;
@@ -477,8 +539,15 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
         if (p.bias) v += p.bias[n];
         if (p.beta != 0.f) v += p.beta * yrow[n];
         yrow[n] = v;
-        csum[j] += v;
-        csq[j] += v * v;
+        if (BP && bnp) {
+          const float x = xrow[n];
+          const float gv = (p.brelu && !(__builtin_fmaf(x, bsc[j], bsh[j]) > 0.f)) ? 0.f : v;
+          csum[j] += gv;
+          csq[j] += gv * (x - bmn[j]) * bis[j];
+        } else {
+          csum[j] += v;
+          csq[j] += v * v;
+        }
       }
     }
   }
@@ -514,8 +583,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
         if (p.bias) v += p.bias[n < p.n ? n : 0];
         if (p.beta != 0.f && mok) v += p.beta * *yp;
         if (mok) *yp = v;
-        rsum[q] += mok ? v : 0.f;
-        rsq[q] += mok ? v * v : 0.f;
+        if (BP && bnp) {  // producer BatchNorm partials of remainder channel n
+          const int nc = n < p.n ? n : p.n - 1;
+          const __amdgpu_buffer_rsrc_t bxr = make_rsrc(p.bx, p.bx_bytes);
+          const float x = load1(bxr, mok ? (uint32_t)(pix_of(mm) * p.bx_ps + n) * 4u : kOOB);
+          const float gv =
+              (p.brelu && !(__builtin_fmaf(x, p.bsave[2 * p.n + nc], p.bsave[3 * p.n + nc]) > 0.f))
+                  ? 0.f : v;
+          rsum[q] += mok ? gv : 0.f;
+          rsq[q] += mok ? gv * (x - p.bsave[nc]) * p.bsave[p.n + nc] : 0.f;
+        } else {
+          rsum[q] += mok ? v : 0.f;
+          rsq[q] += mok ? v * v : 0.f;
+        }
       }
     }
   }
@@ -545,15 +625,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
         }
       }
     }
+    // partial row of this workgroup: class-major over the stride-parity classes (z)
+    const int rows = gridDim.x * gridDim.z;
+    const int srow = blockIdx.z * gridDim.x + bm;
     if (KS > 1) {  // wave 0 holds the whole row tile
       if (g == 0) {
-        const int rows = gridDim.x;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + j * 16 + r;
           if (n >= p.n) continue;
-          p.stats[bm * p.n + n] = csum[j];
-          p.stats[(rows + bm) * p.n + n] = csq[j];
+          p.stats[srow * p.n + n] = csum[j];
+          p.stats[(rows + srow) * p.n + n] = csq[j];
         }
       }
       return;
@@ -566,13 +648,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemm pin) {
       }
     }
     __syncthreads();
-    const int rows = gridDim.x;
     for (int c = threadIdx.x; c < BN + NR; c += 256) {
       if (n0 + c >= p.n) continue;
       float s = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
       float s2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-      p.stats[bm * p.n + n0 + c] = s;
-      p.stats[(rows + bm) * p.n + n0 + c] = s2;
+      p.stats[srow * p.n + n0 + c] = s;
+      p.stats[(rows + srow) * p.n + n0 + c] = s2;
     }
   }
 }
@@ -602,6 +683,12 @@ struct Gemm1 {
   float* stats;         // [2][gridDim.x][n] or null
   uint32_t a_bytes, w_bytes;
   int vec;              // y 16-byte aligned with y_ps % 4 == 0 (else 4-byte stores)
+  // data gradient with bx set (round 6): stats receives the producer BatchNorm's backward
+  // partials (sum g, sum g*xhat; g = y masked by the ReLU recomputed from bx), as IGemm
+  const float* bx;
+  int bx_ps, brelu;
+  const float* bsave;
+  uint32_t bx_bytes;
 };
 
 template <int TM, int TN>
@@ -644,6 +731,17 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  const bool bnp = p.bx != nullptr;
+  float pmn[TN], pis[TN], psc[TN], psh[TN];  // the producer BatchNorm's coefficients
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + j * 16 + r < p.n ? n0 + j * 16 + r : p.n - 1;
+    pmn[j] = bnp ? p.bsave[n] : 0.f;
+    pis[j] = bnp ? p.bsave[p.n + n] : 0.f;
+    psc[j] = bnp ? p.bsave[2 * p.n + n] : 0.f;
+    psh[j] = bnp ? p.bsave[3 * p.n + n] : 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t bxr = make_rsrc(p.bx, bnp ? p.bx_bytes : 0u);
   __syncthreads();  // W staged
 
   auto load = [&](f4* fa, int st) {
@@ -692,7 +790,29 @@ __global__ __launch_bounds__(256) void gemm1x1_kernel(Gemm1 p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mb = t * 16 * TM + i * 16 + 4 * g;
-      if (p.stats) {
+      if (p.stats && bnp) {  // producer BatchNorm partials: one batch of range-checked loads
+        float xv[4][TN];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + j * 16 + r;
+            xv[e][j] = load1(bxr, mb + e < p.M && n < p.n
+                                      ? (uint32_t)((mb + e) * p.bx_ps + n) * 4u : kOOB);
+          }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const bool ok = mb + e < p.M && n0 + j * 16 + r < p.n;
+            const float v = acc[i][j][e];
+            const float x = xv[e][j];
+            const float gv = (p.brelu && !(__builtin_fmaf(x, psc[j], psh[j]) > 0.f)) ? 0.f : v;
+            csum[j] += ok ? gv : 0.f;
+            csq[j] += ok ? gv * (x - pmn[j]) * pis[j] : 0.f;
+          }
+        }
+      } else if (p.stats) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
 #pragma unroll
@@ -1480,7 +1600,9 @@ static bool gemm1_pick(const vae2_act* ad, const vae2_act* yd, int k, int stride
 int launch_igemm(IGemm& p, int role, hipStream_t s, const char* fn, int ncls = 1);
 int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
-                 const G1Tile& t, hipStream_t s, const char* fn);
+                 const G1Tile& t, hipStream_t s, const char* fn, const float* bx = nullptr,
+                 int bx_ps = 0, int brelu = 0, const float* bsave = nullptr,
+                 uint32_t bx_bytes = 0);
 
 
 #if VAE2_PART(1)
@@ -2301,12 +2423,14 @@ int gemm1_blocks_per_cu(int tm, int tn, size_t lds) {
 
 int launch_gemm1(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,
                  const float* bias, float* y, const vae2_act* yd, float beta, float* stats,
-                 const G1Tile& t, hipStream_t s, const char* fn) {
+                 const G1Tile& t, hipStream_t s, const char* fn, const float* bx, int bx_ps,
+                 int brelu, const float* bsave, uint32_t bx_bytes) {
   // (16-byte stores of whole channel quads where y is aligned, 4-byte stores otherwise, so
   // the statistics rows vae2_conv2d_fwd_stats_rows reports do not depend on y's alignment;
   // statistics are of the fresh output only)
   if (stats && beta != 0.f) return -1;
   Gemm1 p{};
+  p.bx = bx; p.bx_ps = bx_ps; p.brelu = brelu; p.bsave = bsave; p.bx_bytes = bx_bytes;
   p.vec = vec_ok(y, (int)yd->ps) ? 1 : 0;
   p.a = a; p.a_ps = (int)ad->ps; p.a_c = (int)ad->c; p.a_c4 = round_up((int)ad->c, 4);
   p.M = (int)act_pixels(yd);
@@ -3048,11 +3172,24 @@ int vae2_conv2d_fwd_bnin(const float* x, const vae2_act* xd, const float* bn_sav
                       bias, y, yd, beta, stats, false, as_stream(stream), fn, bn);
 }
 
+static int igemm_dgrad_setup(IGemm& p, const float* dy, const vae2_act* dyd, const float* wp,
+                             float* dx, const vae2_act* dxd, int k, int stride, int pad,
+                             float beta);
+static int64_t igemm_dgrad_rows(const float* dy, const vae2_act* dyd, const vae2_act* dxd,
+                                int k, int stride, int pad);
+
+// Round 6: every data-gradient kernel family writes the partials -- the direct 3x3 kernels
+// (round 3), the persistent 1x1 GEMM and the gather kernel (every other conv, incl. the
+// stride-2 classes) -- so the rows follow vae2_conv2d_bwd_data's own dispatch.
 int64_t vae2_conv2d_bwd_data_bnpart_rows(const float* dy, const vae2_act* dyd,
                                          const vae2_act* dxd, int k, int stride, int pad) {
   if (!dy || !conv_shapes_ok(dxd, dyd, k, stride, pad) || !fits32(dxd) || !fits32(dyd))
     return 0;
-  return !g_bf16 && dconv_use(dyd, dxd, k, stride, pad, dy) ? dconv_rows(dyd, dxd) : 0;
+  if (g_bf16) return 0;
+  if (dconv_use(dyd, dxd, k, stride, pad, dy)) return dconv_rows(dyd, dxd);
+  G1Tile g1;
+  if (gemm1_pick(dyd, dxd, k, stride, pad, dy, &g1)) return g1.grid_x;
+  return igemm_dgrad_rows(dy, dyd, dxd, k, stride, pad);
 }
 
 int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const float* wp,
@@ -3066,15 +3203,37 @@ int vae2_conv2d_bwd_data_bnpart(const float* dy, const vae2_act* dyd, const floa
                bn_xd->c == dxd->c && bn_xd->ps >= bn_xd->c && fits32(bn_xd), fn,
                "BatchNorm input shape must match dx");
   VAE2_REQUIRE(vae2_conv2d_bwd_data_bnpart_rows(dy, dyd, dxd, k, stride, pad) > 0, fn,
-               "BatchNorm partials need the direct 3x3 kernel (vae2_conv2d_bwd_data_bnpart_rows)");
-  BnSide bn;
-  bn.bx = bn_x;
-  bn.bx_ps = (int)bn_xd->ps;
-  bn.bx_bytes = act_bytes(bn_xd);
-  bn.bsave = bn_save;
-  bn.brelu = relu ? 1 : 0;
-  return launch_dconv(dy, dyd, wp, (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4),
-                      nullptr, dx, dxd, 0.f, partials, true, as_stream(stream), fn, bn);
+               "BatchNorm partials are not available for this geometry "
+               "(vae2_conv2d_bwd_data_bnpart_rows)");
+  const uint32_t wbytes = (uint32_t)(vae2_conv2d_packed_size(dyd->c, dxd->c, k, 1) * 4);
+  if (dconv_use(dyd, dxd, k, stride, pad, dy)) {
+    BnSide bn;
+    bn.bx = bn_x;
+    bn.bx_ps = (int)bn_xd->ps;
+    bn.bx_bytes = act_bytes(bn_xd);
+    bn.bsave = bn_save;
+    bn.brelu = relu ? 1 : 0;
+    return launch_dconv(dy, dyd, wp, wbytes, nullptr, dx, dxd, 0.f, partials, true,
+                        as_stream(stream), fn, bn);
+  }
+  G1Tile g1;
+  if (gemm1_pick(dyd, dxd, k, stride, pad, dy, &g1)) {
+    const int rc = launch_gemm1(dy, dyd, wp, wbytes, nullptr, dx, dxd, 0.f, partials, g1,
+                                as_stream(stream), fn, bn_x, (int)bn_xd->ps, relu ? 1 : 0,
+                                bn_save, act_bytes(bn_xd));
+    VAE2_REQUIRE(rc != -1, fn, "1x1 GEMM refused the partials form");
+    return rc;
+  }
+  IGemm p{};
+  const int ncls = igemm_dgrad_setup(p, dy, dyd, wp, dx, dxd, k, stride, pad, 0.f);
+  VAE2_REQUIRE(ncls > 0, fn, "stride > 2 is not supported");
+  p.stats = partials;
+  p.bx = bn_x;
+  p.bx_ps = (int)bn_xd->ps;
+  p.bx_bytes = act_bytes(bn_xd);
+  p.bsave = bn_save;
+  p.brelu = relu ? 1 : 0;
+  return launch_igemm(p, 1, as_stream(stream), fn, ncls);
 }
 
 int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
@@ -3094,11 +3253,22 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
                                 nullptr, dx, dxd, beta, nullptr, g1, as_stream(stream), fn);
     if (rc != -1) return rc;
   }
+  IGemm p{};
+  const int ncls = igemm_dgrad_setup(p, dy, dyd, wp, dx, dxd, k, stride, pad, beta);
+  VAE2_REQUIRE(ncls >= 0, fn, "stride > 2 is not supported");
+  if (ncls == 0) return 0;
+  return launch_igemm(p, 1, as_stream(stream), fn, ncls);
+}
+
+// The gather kernel's data-gradient setup (vae2_conv2d_bwd_data, the _bnpart form and its
+// rows query): returns the number of stride-parity classes (0: nothing to do, -1: stride > 2).
+static int igemm_dgrad_setup(IGemm& p, const float* dy, const vae2_act* dyd, const float* wp,
+                             float* dx, const vae2_act* dxd, int k, int stride, int pad,
+                             float beta) {
   // Stride-parity classes (ph, pw) of the input pixels: input row ih = stride*i + ph
   // receives from output row oh = (ih + pad - kh)/stride for every kh with
   // (ph + pad - kh) % stride == 0.  All classes run in one launch (class = blockIdx.z);
   // each has only its valid taps.
-  IGemm p{};
   p.a = dy; p.a_ps = (int)dyd->ps; p.a_c = (int)dyd->c; p.a_c4 = round_up((int)dyd->c, 4);
   p.a_h = (int)dyd->h; p.a_w = (int)dyd->w;
   p.g_n = (int)dxd->n;
@@ -3119,7 +3289,7 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
       int gh = (int)((dxd->h - ph + stride - 1) / stride);
       int gw = (int)((dxd->w - pw + stride - 1) / stride);
       if (gh <= 0 || gw <= 0) continue;
-      VAE2_REQUIRE(ncls < 4, fn, "stride > 2 is not supported");
+      if (ncls >= 4) return -1;
       int kh0 = ((ph + pad) % stride + stride) % stride;
       int kw0 = ((pw + pad) % stride + stride) % stride;
       int nth = kh0 < k ? (k - 1 - kh0) / stride + 1 : 0;
@@ -3141,7 +3311,25 @@ int vae2_conv2d_bwd_data(const float* dy, const vae2_act* dyd, const float* wp,
     p.dh0 = c.dh0; p.dw0 = c.dw0; p.kh0 = c.kh0; p.kw0 = c.kw0;
     p.y_offh = c.y_offh; p.y_offw = c.y_offw;
   }
-  return launch_igemm(p, 1, as_stream(stream), fn, ncls);
+  return ncls;
+}
+
+// Partial-statistics rows of a gather-kernel data gradient (gridDim.x * classes).
+static int64_t igemm_dgrad_rows(const float* dy, const vae2_act* dyd, const vae2_act* dxd,
+                                int k, int stride, int pad) {
+  IGemm p{};
+  const int ncls = igemm_dgrad_setup(p, dy, dyd, nullptr, nullptr, dxd, k, stride, pad, 0.f);
+  if (ncls <= 0) return 0;
+  int64_t M = (int64_t)p.g_n * p.g_h * p.g_w;
+  int max_taps = p.nth * p.ntw;
+  for (int c = 0; c < ncls && ncls > 1; ++c) {
+    const IGemm::Cls& q = p.cls[c];
+    const int64_t mc = (int64_t)p.g_n * q.g_h * q.g_w;
+    if (mc > M) M = mc;
+    if (q.nth * q.ntw > max_taps) max_taps = q.nth * q.ntw;
+  }
+  const Tile t = pick_igemm_tile(M, p.n, max_taps, p.a_c4, ncls);
+  return ceil_div(M, igemm_rows_per_block(t)) * ncls;
 }
 
 #endif  // VAE2_PART(0)

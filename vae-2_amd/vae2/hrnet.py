@@ -89,35 +89,41 @@ class Bottleneck(nn.Module):
     def run(self, x):
         link = ops.GradLink(2)  # x feeds conv1 and the shortcut (see BasicBlock.run)
         # bn1's normalised output feeds only conv2 (3x3): normalised in conv2's staging
-        # where the direct 3x3 kernels run (ops.LazyBN, as in run_blocks_lockstep)
-        out = _lazy_pair(x, self.conv1, self.bn1, self.conv2, self.bn2, x_link=link)
+        # where the direct 3x3 kernels run (ops.LazyBN, as in run_blocks_lockstep); bn2's
+        # feeds only conv3 (1x1): its backward partials come from conv3's data gradient
+        pb = ops.PartBN() if ops.PART_BN else None
+        out = _lazy_pair(x, self.conv1, self.bn1, self.conv2, self.bn2, x_link=link, part=pb)
         if self.downsample is None:
-            return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=x, res_link=link)
+            return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=x, res_link=link,
+                               bn_part=pb)
         if len(self.downsample) == 2:  # conv + BN: its output is only bn3's residual (ops.ResBN)
             return ops.conv_bn_multi([out, x], [self.conv3, self.downsample[0]],
                                      [self.bn3, self.downsample[1]], [True, False],
-                                     x_links=[None, link], res_bns=[1, None])[0]
+                                     x_links=[None, link], res_bns=[1, None],
+                                     bn_ins=[pb, None])[0]
         sc = _run_convbn_seq(self.downsample, x, link)
-        return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=sc)
+        return ops.conv_bn(out, self.conv3, self.bn3, relu=True, residual=sc, bn_part=pb)
 
 
 BLOCKS = {"BASIC": BasicBlock, "BOTTLENECK": Bottleneck}
 
 
-def _lazy_pair(x, conv_a, bn_a, conv_b, bn_b, x_link=None):
+def _lazy_pair(x, conv_a, bn_a, conv_b, bn_b, x_link=None, part=None):
     """relu(bn_b(conv_b(relu(bn_a(conv_a(x)))))) where bn_a's output feeds only conv_b: with
     the direct 3x3 kernels for conv_b it is never stored (ops.LazyBN) -- the Bottleneck's
-    bn1 -> conv2 (enc_hrnet.py:84-90) and the stem's bn1 -> conv2 (:788-793)."""
+    bn1 -> conv2 (enc_hrnet.py:84-90) and the stem's bn1 -> conv2 (:788-793); otherwise its
+    backward partials come from conv_b's data gradient (ops.PartBN).  part: bn_b's PartBN
+    (its output's only consumer takes it as bn_part), or None."""
     n, h, w, _ = x.shape
     spec = ops.ConvSpec(conv_a)
     oh, ow = spec.out_hw(h, w)
     lz = ops.LazyBN() if ops.lazy_bn_ok((n, oh, ow, conv_a.out_channels), conv_b) else None
-    if lz is None:
-        out = ops.conv_bn(x, conv_a, bn_a, relu=True, x_link=x_link)
-        return ops.conv_bn(out, conv_b, bn_b, relu=True)
+    if lz is None and ops.PART_BN:
+        lz = ops.PartBN()
     lazy = [lz]
     out = ops.conv_bn_multi([x], [conv_a], [bn_a], True, x_links=[x_link], bn_outs=lazy)
-    return ops.conv_bn_multi(out, [conv_b], [bn_b], True, bn_ins=lazy)[0]
+    return ops.conv_bn_multi(out, [conv_b], [bn_b], True, bn_ins=lazy,
+                             bn_outs=[part] if part is not None else None)[0]
 
 
 def _run_convbn_seq(seq, x, x_link=None):
@@ -125,14 +131,16 @@ def _run_convbn_seq(seq, x, x_link=None):
     return ops.conv_bn(x, seq[0], seq[1], relu=len(seq) > 2, x_link=x_link)
 
 
-def _run_convbn_seqs(seqs, xs, x_links=None, bn_outs=None):
+def _run_convbn_seqs(seqs, xs, x_links=None, bn_outs=None, bn_ins=None):
     """Independent Sequential(Conv2d, BatchNorm2d[, ReLU]) units of one depth level,
     their BatchNorm steps in shared launches (ops.conv_bn_multi).  bn_outs: per unit a
-    LazyBN whose output is handed over un-normalised (set to None where it is stored)."""
+    LazyBN whose output is handed over un-normalised (set to None where it is stored), or a
+    PartBN (output stored, partials from the consumer); bn_ins: the producers' markers."""
     if not seqs:
         return []
     return ops.conv_bn_multi(xs, [q[0] for q in seqs], [q[1] for q in seqs],
-                             [len(q) > 2 for q in seqs], x_links=x_links, bn_outs=bn_outs)
+                             [len(q) > 2 for q in seqs], x_links=x_links, bn_outs=bn_outs,
+                             bn_ins=bn_ins)
 
 
 def run_blocks_lockstep(blocks, xs):
@@ -144,8 +152,11 @@ def run_blocks_lockstep(blocks, xs):
     # bn1's normalised output feeds only conv2: conv2 normalises it while staging its input
     # (ops.LazyBN) where the direct 3x3 kernels run, so it is never stored
     res_ok = all(ops._bn_quad_ok(x) for x in xs)
+    # (elsewhere -- the 144-channel branch, whose conv2 is a gather-kernel conv -- bn1's
+    # output is stored and conv2's data gradient writes its partials: ops.PartBN)
     lazy = [ops.LazyBN() if res_ok and ops.lazy_bn_ok(tuple(x.shape[:3]) + (b.conv1.out_channels,),
-                                                      b.conv2) else None
+                                                      b.conv2) else
+            (ops.PartBN() if ops.PART_BN else None)
             for b, x in zip(blocks, xs)]
     outs = ops.conv_bn_multi(xs, [b.conv1 for b in blocks], [b.bn1 for b in blocks], True,
                              x_links=links, bn_outs=lazy)
@@ -267,15 +278,24 @@ class HighResolutionModule(nn.Module):
             terms[(i, j)], lazy[(i, j)] = t, lz
         downs = [(i, j) for i, _ in rows for j in range(nb) if j < i]
         cur = {(i, j): xs[j] for i, j in downs}
+        parts = {}  # the inner units' PartBN markers, by chain, for the next unit's call
         for k in range(max((i - j for i, j in downs), default=0)):
             live = [(i, j) for i, j in downs if k < i - j]
-            lz_dn = [ops.LazyBN() if ops.FUSE_LAZY and k == i - j - 1 else None for i, j in live]
+            # the last unit's output is normalised by the fuse sum (LazyBN); an inner unit's
+            # (conv + BN + ReLU, stored) feeds only the next stride-2 conv (PartBN)
+            lz_dn = [ops.LazyBN() if ops.FUSE_LAZY and k == i - j - 1 else
+                     (ops.PartBN() if ops.PART_BN and k < i - j - 1 else None)
+                     for i, j in live]
+            ins = [parts.get(ij) for ij in live]
             outs = _run_convbn_seqs([self.fuse_layers[i][j][k] for i, j in live],
                                     [cur[ij] for ij in live],
-                                    [links[j] if k == 0 else None for _, j in live], lz_dn)
+                                    [links[j] if k == 0 else None for _, j in live], lz_dn,
+                                    bn_ins=ins if any(b is not None for b in ins) else None)
+            parts = {ij: lz for ij, lz in zip(live, lz_dn) if isinstance(lz, ops.PartBN)}
             cur.update(zip(live, outs))
-            lazy.update((ij, lz) for ij, lz in zip(live, lz_dn) if lz is not None or
-                        k == ij[0] - ij[1] - 1)
+            lazy.update((ij, lz) for ij, lz in zip(live, lz_dn)
+                        if not isinstance(lz, ops.PartBN) and (lz is not None or
+                                                               k == ij[0] - ij[1] - 1))
         terms.update(cur)
         out = []
         for i, _ in rows:

@@ -155,6 +155,26 @@ class LazyBN:
 LAZY_BN = True  # False: every BatchNorm output is stored (A/B and parity tests)
 
 
+class PartBN:
+    """A training-mode BatchNorm(+ReLU) layer without residual whose STORED output y feeds
+    exactly one conv that cannot normalise lazily (a 1x1 GEMM, a gather-kernel conv, a
+    stride-2 conv): the Bottleneck's bn2 -> conv3 (enc_hrnet.py:84-101), the 144-channel
+    branch's BasicBlock bn1 -> conv2, the inner units of a fuse down-chain (:199-218).  The
+    forward is unchanged; the consumer's data gradient -- the gradient of y, complete because
+    y has no other consumer -- writes this layer's backward partials (sum g, sum g*xhat) in
+    its epilogue (vae2_conv2d_bwd_data_bnpart, every kernel family since round 6), so the
+    layer's backward reduce pass does not run.  r = the layer's pre-BN tensor (the ReLU mask
+    is recomputed from it), save = its (mean, invstd, scale, shift)."""
+
+    __slots__ = ("save", "relu", "part", "rows", "r")
+
+    def __init__(self):
+        self.save, self.relu, self.part, self.rows, self.r = None, False, None, 0, None
+
+
+PART_BN = True  # False: the layers above run their own backward reduce pass (A/B, tests)
+
+
 class ResBN:
     """Marks a layer of a _ConvBNMulti level whose BatchNorm output (no ReLU) is only the
     residual of another layer of the same level (the Bottleneck's downsample shortcut,
@@ -192,7 +212,7 @@ class ConvSpec:
     """Static description of a conv(+BN) call: geometry and module handles."""
 
     __slots__ = ("k", "stride", "pad", "relu", "bn", "momentum", "eps", "training", "x_link",
-                 "res_link", "bn_in", "bn_out", "res_bn")
+                 "res_link", "bn_in", "bn_out", "res_bn", "bn_part")
 
     def __init__(self, conv, bn=None, relu=False):
         kh, kw = conv.kernel_size
@@ -205,6 +225,7 @@ class ConvSpec:
         self.bn = bn
         self.x_link = self.res_link = None
         self.bn_in = self.bn_out = None  # LazyBN: BatchNorm fused into the consumer conv
+        self.bn_part = None  # PartBN of the producer of x: partials from this conv's dgrad
         self.res_bn = None  # index (in its level) of the layer whose BN output is the residual
         if bn is not None:
             if bn.momentum is None:
@@ -582,18 +603,24 @@ def _conv_bwd(x, weight, bias, dy, spec, need_dx, need_w=True, need_b=True, grou
         if prof.active():
             _conv_work("dgrad", xa, tuple(dy.shape), spec.k, spec.stride)
         lz = spec.bn_in
+        pb = spec.bn_part
+        if pb is not None and (pb.r is None or pb.save is None or link is not None):
+            pb = None  # the producer stored no pre-BN tensor, or x has another consumer
         rows = 0
-        if lz is not None and beta == 0.0:
+        if (lz is not None or pb is not None) and beta == 0.0:
             rows = _lib.load().vae2_conv2d_bwd_data_bnpart_rows(
                 dyp, ctypes.byref(dya), ctypes.byref(dxa), spec.k, spec.stride, spec.pad)
-        if rows > 0:  # + the LazyBN layer's backward partials (its reduce pass skipped)
+        if rows > 0:  # + the producer layer's backward partials (its reduce pass skipped)
             part = _empty((2 * rows * xa.c,), x)
             if hold is not None:
                 hold.append(part)
+            src = lz if lz is not None else pb
+            # the producer's pre-BN tensor: x itself for a LazyBN input, r for a PartBN one
+            bxp, bxa = (xp, xa) if lz is not None else act_of(pb.r)
             call("vae2_conv2d_bwd_data_bnpart", dyp, ctypes.byref(dya), ptr(wp), dxp,
-                 ctypes.byref(dxa), spec.k, spec.stride, spec.pad, xp, ctypes.byref(xa),
-                 ptr(lz.save), int(lz.relu), ptr(part), s)
-            lz.part, lz.rows = part, rows
+                 ctypes.byref(dxa), spec.k, spec.stride, spec.pad, bxp, ctypes.byref(bxa),
+                 ptr(src.save), int(src.relu), ptr(part), s)
+            src.part, src.rows = part, rows
         elif group is not None:
             group.add(1, dyp, dya, wp, None, dxp, dxa, spec, beta)
         else:
@@ -720,13 +747,15 @@ class _ConvBN(torch.autograd.Function):
         return dx, wret, bret_conv, gret, bret, dres, None
 
 
-def conv_bn(x, conv, bn, relu, residual=None, x_link=None, res_link=None):
+def conv_bn(x, conv, bn, relu, residual=None, x_link=None, res_link=None, bn_part=None):
     """relu?(bn(conv(x)) + residual) with training-mode (or eval-mode) BatchNorm.
     x_link / res_link: GradLink shared with the other consumer(s) of x / residual.
-    Training mode goes through the multi-layer path (one layer); eval mode, and
+    bn_part: the PartBN of the layer that produced x (its partials from this conv's data
+    gradient).  Training mode goes through the multi-layer path (one layer); eval mode, and
     residual views the multi-layer kernels cannot take, through _ConvBN."""
     spec = ConvSpec(conv, bn, relu)
     spec.x_link, spec.res_link = x_link, res_link
+    spec.bn_part = bn_part if PART_BN else None
     if spec.training and (residual is None or _bn_quad_ok(residual)):
         return _ConvBNMulti.apply((spec,), x, conv.weight, conv.bias, bn.weight, bn.bias,
                                   residual)[0]
@@ -892,6 +921,11 @@ class _ConvBNMulti(torch.autograd.Function):
             if isinstance(lz, ResBN):  # added by its consumer's apply: r stands in for y
                 ys.append(r)
                 continue
+            if isinstance(lz, PartBN):  # y stored as usual; the consumer's data gradient
+                ok = L[i][5] is None and spec.res_bn is None  # will write the partials
+                lz.save, lz.relu, lz.part, lz.rows = save, spec.relu, None, 0
+                lz.r = r if ok else None
+                lz = None
             if lz is not None:  # normalised by the consumer conv: r stands in for y
                 lz.save, lz.relu, lz.part, lz.rows = save, spec.relu, None, 0
                 ys.append(r)
@@ -1125,6 +1159,8 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
     that takes it lazily -- the returned tensor is then the pre-BN conv output, to be
     passed on with bn_ins[i] = that LazyBN to the consumer's conv_bn_multi call.  Where
     the batched path does not run, the entry is set to None (the output is stored).
+    A PartBN entry instead keeps the stored output and, passed on as the consumer's
+    bn_ins[i], makes the consumer's data gradient write layer i's backward partials.
 
     res_bns[i] (an index j, or None): layer i's residual is layer j's BatchNorm output
     (layer j: no ReLU, no residual of its own, same output shape), added in layer i's
@@ -1142,7 +1178,10 @@ def conv_bn_multi(xs, convs, bns, relu, residuals=None, x_links=None, res_links=
         if bn_outs is not None:
             spec.bn_out = bn_outs[i]
         if bn_ins is not None:
-            spec.bn_in = bn_ins[i]
+            if isinstance(bn_ins[i], PartBN):  # stored input, partials from the dgrad
+                spec.bn_part = bn_ins[i] if PART_BN else None
+            else:
+                spec.bn_in = bn_ins[i]
         specs.append(spec)
     if res_bns is not None:
         for i, j in enumerate(res_bns):
