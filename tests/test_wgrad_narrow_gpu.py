@@ -80,9 +80,11 @@ def test_wgrad_narrow_matches_fp64(shape):
     dw_old, names_old = _run(x, dy, 0)
     assert not any(k.startswith("wgrad3n_kernel") for k in names_old), names_old
     assert rel(dw, dw_old) < 1e-5
-    # the register-prefetch form (tune key 7 = 2) computes the same sums in the same order
+    # the register-prefetch form (tune key 7 = 2): the same per-tile sums; its occupancy
+    # (140 vs 112 VGPRs for 18 channels) can give another split plan, i.e. another order of
+    # the partial-slab sum
     dw_pf, _ = _run(x, dy, 2)
-    assert torch.equal(dw, dw_pf)
+    assert rel(dw_pf, dw) < 1e-5
     # the 8-wave form (key 7 = 3: the extra waves split the pixel chunks, summed through
     # LDS in wave order): the same sums in another order
     dw_8, names_8 = _run(x, dy, 3)

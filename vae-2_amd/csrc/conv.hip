@@ -978,7 +978,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
   const int trem = bm - img * per_img;
   const int th = trem / p.tiles_w;
   const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * kDcBW;
-  const int n0 = by * BN;
+  const int n0 = by * BNT;  // (NR > 0 with two N blocks: 72 = 2 x (32 + 4), set_tune key 14)
   const int kk4 = 9 * p.a_c4;
   const int csp = p.cs4 * 4 + 4;  // LDS floats per pixel (+4: bank spread)
   const int Q = p.a_c4 >> 2;
@@ -1500,11 +1500,12 @@ int g_wgrad_narrow = 3;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18
                           //  18 / 36 / 72 ch 35.0 / 31.7 / 32.1 -> 33.0 / 31.4 / 31.2 us)
 int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-step table
 int g_dconv_n16 = 0;      // vae2_conv2d_set_tune key 13: direct 3x3 16-channel N blocks when short of workgroups
+int g_dconv_split72 = 0;  // vae2_conv2d_set_tune key 14: 72-channel direct 3x3 as two 32 + 4 N blocks
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
-    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab, g_dconv_n16;
+    g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab, g_dconv_n16, g_dconv_split72;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2524,6 +2525,14 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
     d.tn = 1;
     d.nblk = (N + 15) / 16;
   }
+  // tune key 14: the 72-channel branch as two N blocks of 32 MFMA + 4 VALU channels
+  // (block b: channels 36 b ..) -- the same workgroups as the two padded 48-column blocks
+  // (24 of their 96 MFMA columns are padding), a third fewer MFMAs per block
+  if (remainder && g_dconv_split72 && g_dconv_nr && !g_bf16 && d.nr == 0 && N == 72 &&
+      d.nblk == 2 && d.tn == 3) {
+    d.tn = 2;
+    d.nr = 4;
+  }
   return d;
 }
 
@@ -2960,6 +2969,11 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels
     const int prev = g_dconv_stream;
     g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
+    return prev;
+  }
+  if (key == 14) {  // direct 3x3: 72 channels as two 32 + 4 N blocks
+    const int prev = g_dconv_split72;
+    g_dconv_split72 = value ? 1 : 0;
     return prev;
   }
   if (key == 13) {  // direct 3x3: 16-channel N blocks for layers short of workgroups

@@ -63,6 +63,12 @@ __global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
   constexpr int DP = 4 * COQ;                    // dY floats per pixel in LDS
   constexpr int XP = CSW;                        // X floats per halo pixel in LDS
   constexpr int LPX = (kTH + 2) * kLW;           // halo pixels
+  // LDS floats per halo row: padded to = CSW (mod 16), so the 16 columns of a group -- (dh, ci)
+  // runs crossing a dh boundary -- fall on 16 distinct banks mod 16; lane groups g and g + 1
+  // are 4 pixels = 16 banks apart (4 XP = 16 mod 32), so a 32-lane half of a ds_read_b32
+  // hits 32 distinct banks (the unpadded rows, = 8 mod 16, made 2-way conflicts in every
+  // group that crosses a row)
+  constexpr int RS = kLW * XP + ((CSW - kLW * XP) % 16 + 16) % 16;
   constexpr int G = (3 * CSW + 15) / 16;         // 16-column groups per dw
   constexpr int WCOL = NW / WPIX;
   constexpr int NT = 64 * NW;
@@ -70,8 +76,8 @@ __global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
   static_assert(NR <= 4 && (NR == 0 || COQ == 4 * TM + 1), "one remainder quad");
   static_assert(WCOL * WPIX == NW && (WCOL == 1 || WCOL == 2 || WCOL == 4), "waves per tile");
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* xs = sm;                   // [LPX][XP]
-  float* ds = sm + LPX * XP;        // [kNPX][DP]
+  float* xs = sm;                   // [kTH + 2][RS]: halo rows of kLW pixels x XP
+  float* ds = sm + (kTH + 2) * RS;  // [kNPX][DP]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r = lane & 15;
@@ -82,15 +88,17 @@ __global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
 
   // this lane's column of each of the wave's groups: halo offset of (dh, ci) (an invalid
-  // column reads a valid address; its sums are never written)
+  // column reads the address of the last real one -- a broadcast, no bank conflict -- and
+  // its sums are never written)
   int xoff[GW];
   bool colok[GW];
 #pragma unroll
   for (int j = 0; j < GW; ++j) {
     const int n = (wc * GW + j) * 16 + r;
-    const int dh = n / CSW, ci = n - dh * CSW;
+    const int nc = n < 3 * CSW ? n : 3 * CSW - 1;
+    const int dh = nc / CSW, ci = nc - dh * CSW;
     colok[j] = wc * GW + j < G && n < 3 * CSW && c0 + ci < p.cin;
-    xoff[j] = colok[j] ? dh * kLW * XP + ci : 0;
+    xoff[j] = dh * RS + ci;
   }
   // input BatchNorm: the slab's scale / shift in LDS (read after the tile loop's first
   // barrier), applied to in-image pixels in the staging (= bn_apply_body's arithmetic)
@@ -172,7 +180,8 @@ __global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
       if (p.isave && ((xin >> u) & 1u)) ibn(v, xq);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = xc + k < p.cin ? v[k] : 0.f;  // channel padding
-      *reinterpret_cast<f4*>(&xs[hp * XP + 4 * xq]) = v;
+      const int lr = hp / kLW, lc = hp - lr * kLW;
+      *reinterpret_cast<f4*>(&xs[lr * RS + lc * XP + 4 * xq]) = v;
     }
 #pragma unroll
     for (int u = 0; u < NDI; ++u) {
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad3n_kernel(WGN p) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) rq[s] = *reinterpret_cast<const f4*>(&ds[(dpx + s) * DP + 16 * TM]);
       }
-      const int xb = (orow * kLW + cb + 4 * g) * XP;
+      const int xb = orow * RS + (cb + 4 * g) * XP;
 #pragma unroll
       for (int j = 0; j < GW; ++j) {
         float xv[6];
@@ -362,7 +371,8 @@ bool pick(const vae2_act* xd, const vae2_act* dyd, Cfg& c) {
 
 size_t lds_bytes(const Cfg& c) {
   const int CO = 16 * c.tm + c.nr, DP = 4 * ((CO + 3) / 4);
-  const size_t stage = ((size_t)(kTH + 2) * kLW * 4 * c.cq + (size_t)kNPX * DP) * sizeof(float);
+  const int csw = 4 * c.cq, rs = kLW * csw + ((csw - kLW * csw) % 16 + 16) % 16;  // = RS
+  const size_t stage = ((size_t)(kTH + 2) * rs + (size_t)kNPX * DP) * sizeof(float);
   const int G = (3 * 4 * c.cq + 15) / 16, wcol = c.nw / c.wpix, gw = (G + wcol - 1) / wcol;
   const size_t nv = (size_t)c.tm * gw * 12 + (size_t)gw * 3 * c.nr;
   const size_t red = c.wpix > 1 ? (size_t)(c.wpix - 1) * wcol * nv * 64 * sizeof(float) : 0;
