@@ -81,7 +81,8 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * (default 4); key 5 = 1: its row tiles of 16 instead of 32 pixels; key 6 = 1: gather-GEMM
  * convs with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder columns); keys
  * 7-13: see vae2_conv2d_set_tune in csrc/conv.hip; key 14 = 1: the 72-channel direct 3x3
- * as two N blocks of 32 + 4 (off: measured slower).  Returns the previous value, -1 for an unknown key or an
+ * as two N blocks of 32 + 4 (off: measured slower); key 15 = 1 (default): direct 3x3
+ * layers whose 4-row tiles leave <= 2 workgroups per CU split K over 8-wave workgroups.  Returns the previous value, -1 for an unknown key or an
  * out-of-range value of keys 4, 6 and 7 (the setting is then left unchanged).          */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every

@@ -1,9 +1,14 @@
-"""The 72-channel direct 3x3 conv as two N blocks of 32 MFMA + 4 VALU channels
-(vae2_conv2d_set_tune key 14; the W18 72-channel branch at 32 x 64, enc_hrnet.py:27-62)
-against fp64 PyTorch and against the two padded 48-column blocks it replaces: forward
-(+ bias, + beta * y, BN partial statistics), forward with the producer BatchNorm applied in
-the staging, data gradient (+ beta) and the data gradient's producer-BatchNorm backward
-partials.  Shapes: the bench layer, a partial strip with H % 4 = 1, a padded input quad."""
+"""Two launch forms of the direct 3x3 conv for layers short of workgroups (the W18 72-channel
+branch at 32 x 64: 256 workgroups, one wave per SIMD; enc_hrnet.py:27-62):
+  split72 (vae2_conv2d_set_tune key 14): 72 channels as two N blocks of 32 MFMA + 4 VALU
+          channels instead of two padded 48-column blocks;
+  ksp     (key 15): the same 4-row tiles as 8-wave workgroups splitting K in two (K chunk
+          pairs alternate between the wave sets, summed through LDS in a fixed order).
+Each against fp64 PyTorch and against the default form: forward (+ bias, + beta * y, BN
+partial statistics), forward with the producer BatchNorm applied in the staging, data
+gradient (+ beta) and the data gradient's producer-BatchNorm backward partials.  Shapes: the
+bench layer, a partial strip with H % 4 = 1, a padded input quad, and (ksp) 64 / 32 channels
+(4 / 2 column tiles)."""
 import ctypes
 
 import pytest
@@ -16,11 +21,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 SHAPES = [
-    # N, H, W, Cin, Cout (auto dispatch: the direct kernel, 128-255 tiles, two N blocks)
+    # N, H, W, Cin, Cout (auto dispatch: the direct kernel, 256-511 workgroups)
     (8, 32, 64, 72, 72),   # the bench layer
     (6, 29, 80, 72, 72),   # partial strip, H % 4 = 1
     (6, 32, 72, 70, 72),   # padded input channel quad
+    (8, 32, 128, 64, 64),  # ksp only: one N block of 4 tiles
+    (8, 32, 128, 32, 32),  # ksp only: 2 tiles
 ]
+KEY = {"split72": 14, "ksp": 15}
 
 
 def _lib():
@@ -28,33 +36,48 @@ def _lib():
     return _lib.load()
 
 
-def _split(on):
-    return _lib().vae2_conv2d_set_tune(14, 1 if on else 0)
-
-
-@pytest.fixture(autouse=True)
-def _algo():
+@pytest.fixture(params=["split72", "ksp"])
+def form(request):
     lib = _lib()
     prev = lib.vae2_conv2d_set_algo(0)
-    prev14 = lib.vae2_conv2d_set_tune(14, 1)
-    yield
-    lib.vae2_conv2d_set_tune(14, prev14)
+    prevs = {k: lib.vae2_conv2d_set_tune(k, 0) for k in KEY.values()}
+    lib.vae2_conv2d_set_tune(KEY[request.param], 1)
+    yield request.param
+    for k, v in prevs.items():
+        lib.vae2_conv2d_set_tune(k, v)
     lib.vae2_conv2d_set_algo(prev)
 
 
-def _form(names, flip):
-    """(2, 4) for the split form, (3, 0) for the padded blocks, from the dconv3 instance."""
+def _switch(form, on):
+    _lib().vae2_conv2d_set_tune(KEY[form], 1 if on else 0)
+
+
+def _skip(form, shape):
+    if form == "split72" and shape[4] != 72:
+        pytest.skip("72 output channels only")
+
+
+def _args(names, flip):
+    """Template arguments of the one dconv3 instance of the direction."""
     tag = "true" if flip else "false"
     args = [[s.strip() for s in k[len("dconv3_kernel<"):k.index(">")].split(",")]
             for k in names if k.startswith("dconv3_kernel<")]
     args = [a for a in args if a[2] == tag]
     assert len(args) == 1, names
-    a = args[0]
-    return int(a[1]), int(a[4]) if len(a) > 4 else 0
+    return args[0]
+
+
+def _check(form, names, flip, on=True):
+    a = _args(names, flip)
+    if form == "split72":
+        assert (int(a[1]), int(a[4])) == ((2, 4) if on else (3, 0)), a
+    else:
+        assert (a[6:8] == ["8", "true"]) == on and int(a[4]) == 0, a
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_split72_forward_stats(shape):
+def test_form_forward_stats(form, shape):
+    _skip(form, shape)
     torch.manual_seed(21)
     n, h, w, cin, cout = shape
     x = torch.randn(n, cin, h, w, device=DEV)
@@ -64,9 +87,9 @@ def test_split72_forward_stats(shape):
     ref = F.conv2d(x.double(), wt.double(), bias.double(), 1, 1)
     outs = {}
     for on in (True, False):
-        _split(on)
+        _switch(form, on)
         y, st, names = _fwd(xg, wt, bias, stats_rows=True)
-        assert _form(names, False) == ((2, 4) if on else (3, 0))
+        _check(form, names, False, on)
         assert rel(_nchw(y), ref) < 1e-6
         assert torch.isfinite(st).all()  # every statistics row written
         sums = st.double().sum(1)
@@ -76,8 +99,9 @@ def test_split72_forward_stats(shape):
     assert outs[True][1] == outs[False][1]  # the same partial-statistics rows
 
 
-@pytest.mark.parametrize("shape", SHAPES[:2])
-def test_split72_forward_beta(shape):
+@pytest.mark.parametrize("shape", SHAPES[:2] + SHAPES[4:])
+def test_form_forward_beta(form, shape):
+    _skip(form, shape)
     torch.manual_seed(22)
     n, h, w, cin, cout = shape
     x = torch.randn(n, cin, h, w, device=DEV)
@@ -85,7 +109,7 @@ def test_split72_forward_beta(shape):
     old = torch.randn(n, cout, h, w, device=DEV)
     ref = F.conv2d(x.double(), wt.double(), None, 1, 1) + 0.5 * old.double()
     y, st, names = _fwd(_nhwc(x), wt, None, y=_nhwc(old), beta=0.5, stats_rows=True)
-    assert _form(names, False) == (2, 4)
+    _check(form, names, False)
     assert rel(_nchw(y), ref) < 1e-6
     sums = st.double().sum(1)
     assert sums_ok(sums[0], ref) and sums_ok(sums[1], ref * ref)
@@ -93,7 +117,8 @@ def test_split72_forward_beta(shape):
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("relu", [0, 1])
-def test_split72_forward_input_bn(shape, relu):
+def test_form_forward_input_bn(form, shape, relu):
+    _skip(form, shape)
     torch.manual_seed(23)
     n, h, w, cin, cout = shape
     x = torch.randn(n, cin, h, w, device=DEV)
@@ -104,7 +129,7 @@ def test_split72_forward_input_bn(shape, relu):
         xb = xb.clamp_min(0)
     ref = F.conv2d(xb, wt.double(), None, 1, 1)
     y, st, names = _fwd(_nhwc(x), wt, None, stats_rows=True, bn_save=sv, relu=relu)
-    assert _form(names, False) == (2, 4)
+    _check(form, names, False)
     assert rel(_nchw(y), ref) < 1e-6
     assert sums_ok(st.double().sum(1)[0], ref)
 
@@ -113,7 +138,8 @@ SQUARE = [s for s in SHAPES if s[3] == s[4]]
 
 
 @pytest.mark.parametrize("shape", SQUARE)
-def test_split72_data_gradient(shape):
+def test_form_data_gradient(form, shape):
+    _skip(form, shape)
     from vae2 import ops
     torch.manual_seed(24)
     n, h, w, cin, cout = shape
@@ -130,7 +156,7 @@ def test_split72_data_gradient(shape):
         ops.call("vae2_conv2d_bwd_data", dyp, ctypes.byref(dya), ops.ptr(wp), dxp,
                  ctypes.byref(dxa), 3, 1, 1, beta, ops.stream_ptr())
     _, names = _names(lambda: run(0.0))
-    assert _form(names, True) == (2, 4)
+    _check(form, names, True)
     assert rel(_nchw(dx), ref) < 1e-6
     run(1.0)
     torch.cuda.synchronize()
@@ -139,7 +165,8 @@ def test_split72_data_gradient(shape):
 
 @pytest.mark.parametrize("shape", SQUARE)
 @pytest.mark.parametrize("relu", [0, 1])
-def test_split72_data_gradient_bn_partials(shape, relu):
+def test_form_data_gradient_bn_partials(form, shape, relu):
+    _skip(form, shape)
     from vae2 import ops
     torch.manual_seed(25)
     n, h, w, cin, cout = shape
@@ -164,7 +191,7 @@ def test_split72_data_gradient_bn_partials(shape, relu):
         "vae2_conv2d_bwd_data_bnpart", dyp, ctypes.byref(dya), ops.ptr(wp), dxp,
         ctypes.byref(dxa), 3, 1, 1, bxp, ctypes.byref(bxa), ops.ptr(sv), relu, ops.ptr(part),
         ops.stream_ptr()))
-    assert _form(names, True) == (2, 4)
+    _check(form, names, True)
     assert rel(_nchw(dx), dxr) < 1e-6
     assert torch.isfinite(part).all()
     sums = part.double().sum(1)
