@@ -72,7 +72,7 @@ int vae2_conv2d_set_algo(int algo);
 int vae2_conv2d_set_mfma_bf16(int on);
 /* Launch-shape tuning knobs for A/B measurements (every setting computes the same
  * result): key 0 = minimum igemm workgroups (row tiles shrink 4 -> 2 -> 1 until the grid
- * reaches it; 0 = the default rule); key 1 = 1: weight gradients with 64 (tap, Cin4)
+ * reaches it; default 512, 0 = the 4-row-tile rule alone); key 1 = 1: weight gradients with 64 (tap, Cin4)
  * columns take 2 x 16 output-channel rows and all 64 columns per workgroup (not 4 x 16
  * rows and 48 + 48 columns); key 2 = 1: the direct 3x3 kernels' 8-row tiles run as 8
  * waves of one row each (512 threads) instead of 4 waves of two rows; key 3 = 1: the

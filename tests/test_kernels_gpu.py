@@ -793,6 +793,7 @@ def test_conv2d_multi_grouped_equals_single_calls():
     lib = _lib.load()
     prev = lib.vae2_conv2d_set_algo(2 + 16)  # (VALU-remainder layers are never grouped)
     prev_g = lib.vae2_conv2d_set_grouping(1)
+    prev_k = lib.vae2_conv2d_set_tune(15, 0)  # (nor the K-split 8-wave form: own launches)
     s = ops.stream_ptr()
     torch.manual_seed(5)
     like = torch.empty(1, device=DEV)
@@ -866,6 +867,7 @@ def test_conv2d_multi_grouped_equals_single_calls():
     finally:
         lib.vae2_conv2d_set_algo(prev)
         lib.vae2_conv2d_set_grouping(prev_g)
+        lib.vae2_conv2d_set_tune(15, prev_k)
     assert any(nm.startswith("dconv3_group_kernel") for nm in names), names
     assert len(names) < 2 * len(MULTI_SHAPES), names  # fewer launches than jobs
     for ta, tb in zip(a, b):

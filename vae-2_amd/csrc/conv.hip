@@ -1511,7 +1511,9 @@ int g_dconv_nr = 1;  // vae2_conv2d_set_algo: bit 16 clear enables the VALU rema
 int g_gemm1 = 1;     // vae2_conv2d_set_algo: bit 32 clear enables the persistent 1x1 GEMM
 int g_vec_out = 1;   // vae2_conv2d_set_algo: bit 64 clear enables the quad-transposed stores
 int g_dconv_nr_wide = 1;  // vae2_conv2d_set_algo: bit 128 clear enables the 32 + 4 / 64 + 8 forms
-int g_igemm_minblk = 0;   // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
+int g_igemm_minblk = 512;  // vae2_conv2d_set_tune key 0: igemm row tiles shrink to reach this grid
+                           // (512 since round 6: step 909.3-910.7 -> 915.4-915.8 frames/s over 3
+                           //  interleaved reps, 768: level; scripts/gpu_r6_q.sh)
 // (keys 1 and 3 on by default: round-4 A/B on one box, 20-step benches twice interleaved:
 //  default 820.7 / 822.4 frames/s, key 1 824.2 / 823.1, key 3 828.3 / 828.3; key 2 (8-wave
 //  direct 3x3) 825.1 / 823.8 and key 0 = 1024 819.7 / 818.4 stay off)
