@@ -264,14 +264,23 @@ def test_stream_rows_match_launch_plan():
         _, st, _ = _fwd(_nhwc(x), wt, None, stats_rows=True)
         assert torch.isfinite(st).all(), shape
     # the query follows set_tune key 9: bands of the streaming plan (2 x 2 strips x 2 bands
-    # of 8 rows) vs the per-tile kernel's 4-row tiles (2 x 4 x 2)
+    # of 8 rows at key 17 = 2: at least 2 steps per band; 4 bands of 4 rows at the default 1)
+    # vs the per-tile kernel's 4-row tiles (2 x 4 x 2)
     xa = ops.Act(2, 13, 40, 18, 20)
     ya = ops.Act(2, 13, 40, 18, 18)
     lib = _lib()
-    r1 = lib.vae2_conv2d_fwd_stats_rows(ctypes.c_void_p(256), ctypes.byref(xa), ctypes.byref(ya), 3, 1, 1)
+    rows = lambda: lib.vae2_conv2d_fwd_stats_rows(ctypes.c_void_p(256), ctypes.byref(xa),
+                                                  ctypes.byref(ya), 3, 1, 1)
+    prev = lib.vae2_conv2d_set_tune(17, 2)
+    try:
+        r2 = rows()
+        lib.vae2_conv2d_set_tune(17, 1)
+        r1 = rows()
+    finally:
+        lib.vae2_conv2d_set_tune(17, prev)
     _stream(False)
-    r0 = lib.vae2_conv2d_fwd_stats_rows(ctypes.c_void_p(256), ctypes.byref(xa), ctypes.byref(ya), 3, 1, 1)
-    assert (r1, r0) == (8, 16)
+    r0 = rows()
+    assert (r2, r1, r0) == (8, 16, 16)
 
 
 @pytest.mark.parametrize("shape", [SHAPES[1], SHAPES[4]])

@@ -3041,6 +3041,18 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
     return prev;
   }
+  if (key == 16) {  // wgrad_narrow.hip: minimum tiles per split (partial slab)
+    if (value < 1 || value > 2) return -1;
+    const int prev = g_wgrad_narrow_tps;
+    g_wgrad_narrow_tps = value;
+    return prev;
+  }
+  if (key == 17) {  // dconv_stream.hip: minimum 4-row steps per band
+    if (value < 1 || value > 2) return -1;
+    const int prev = g_dconv_stream_spb;
+    g_dconv_stream_spb = value;
+    return prev;
+  }
   if (key == 15) {  // direct 3x3: K split over 8 waves for layers short of workgroups
     const int prev = g_dconv_ksp;
     g_dconv_ksp = value ? 1 : 0;

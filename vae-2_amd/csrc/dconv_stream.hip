@@ -42,6 +42,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 int g_dconv_stream = 3;      // vae2_conv2d_set_tune key 9: bit 0 18 channels, bit 1 36 channels
 int g_dconv_stream_wpc = 0;  // vae2_conv2d_set_tune key 10: target workgroups per CU (0 auto)
 int g_dconv_stream_bl = 0;   // vae2_conv2d_set_tune key 11: 18-channel weights in LDS
+int g_dconv_stream_spb = 1;  // vae2_conv2d_set_tune key 17: minimum 4-row steps per band (1 or 2;
+                             // 1 since round 6: the 36-channel layers get 512 one-step bands
+                             // instead of 256 two-step ones, step +0.5 %, scripts/gpu_r6_r.sh, _s.sh)
 
 struct DStream {
   const float* a;
@@ -510,7 +513,7 @@ bool ds_plan(const vae2_act* ad, const vae2_act* yd, DsPlan* pl) {
   const int64_t total = yd->n * d.tiles_w * qsteps;
   const int wpc = g_dconv_stream_wpc > 0 ? g_dconv_stream_wpc : (Q == 5 ? 4 : 2);
   int64_t spb = ceil_div(total, 256LL * wpc);
-  if (spb < 2) spb = 2;
+  if (spb < g_dconv_stream_spb) spb = g_dconv_stream_spb;
   if (spb > qsteps) spb = qsteps;
   d.band_rows = (int)(4 * spb);
   d.nbands = (int)ceil_div(yd->h, d.band_rows);

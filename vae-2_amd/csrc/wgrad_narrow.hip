@@ -25,6 +25,7 @@
 namespace vae2 {
 
 extern int g_bf16, g_wgrad_narrow;
+int g_wgrad_narrow_tps = 2;  // vae2_conv2d_set_tune key 16: minimum tiles per split (1 or 2)
 
 // (the kernel is an exported symbol, outside the anonymous namespace: the launch log
 // names kernels through the dynamic symbol table)
@@ -419,7 +420,7 @@ bool plan(const vae2_act* xd, const vae2_act* dyd, Plan& pl) {
   int64_t want = (int64_t)256 * resident_per_cu(pl.c) / gy;
   if (want < 1) want = 1;
   pl.tps = (int)ceil_div(pl.ntiles, want);
-  if (pl.tps < 2) pl.tps = 2;
+  if (pl.tps < g_wgrad_narrow_tps) pl.tps = g_wgrad_narrow_tps;
   pl.splits = (int)ceil_div(pl.ntiles, pl.tps);
   return true;
 }
