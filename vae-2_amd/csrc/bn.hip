@@ -23,9 +23,11 @@ namespace vae2 {
 // reduce launches streamed at 0.34 of the HBM peak.)
 static inline int quad_rows(int64_t C);
 constexpr int kPassU = 4;  // = kApplyU (defined with the apply kernels below)
+int g_bn_blocks = 1024;  // vae2_conv2d_set_tune key 19: blocks per layer (at most, whole passes)
+
 static int64_t pix_per_block(int64_t P, int64_t C) {
   const int64_t pass = (int64_t)quad_rows(C) * kPassU;
-  const int64_t n = ceil_div(P, 1024 * pass);
+  const int64_t n = ceil_div(P, (int64_t)g_bn_blocks * pass);
   return pass * (n > 0 ? n : 1);
 }
 

@@ -1536,12 +1536,13 @@ int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-st
 int g_dconv_n16 = 0;      // vae2_conv2d_set_tune key 13: direct 3x3 16-channel N blocks when short of workgroups
 int g_dconv_split72 = 0;  // vae2_conv2d_set_tune key 14: 72-channel direct 3x3 as two 32 + 4 N blocks
 int g_dconv_ksp = 1;      // vae2_conv2d_set_tune key 15: direct 3x3 K split over 8 waves when short of workgroups
+int g_wgrad_wgs = 1024;   // vae2_conv2d_set_tune key 18: gather weight-gradient target workgroups
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
 extern int g_wide_tiles, g_ksplit, g_bf16, g_conv_algo, g_dconv_nr, g_gemm1, g_vec_out,
     g_dconv_nr_wide, g_igemm_minblk, g_wgrad_cols, g_dconv_nw8, g_wgrad_nw8, g_gemm1_tn,
     g_gemm1_tm, g_igemm_nr, g_wgrad_narrow, g_igemm_tab, g_dconv_n16, g_dconv_split72,
-    g_dconv_ksp;
+    g_dconv_ksp, g_wgrad_wgs;
 #endif
 
 // 1x1 convs with many output channels ("wide"): up to 9 column tiles per wave and
@@ -2363,10 +2364,10 @@ static WTile pick_wtile(int64_t P, int cout, int ncol4) {
   t.tn = ct <= tn_max ? ct : tn_max;
   t.gx = (int)ceil_div(ncol4, 16 * t.tn);
   int64_t tiles = (int64_t)t.gx * t.gy;
-  // ~1024 workgroups (4 waves each), at least 256 pixels (4 chunks per wave) each: small
-  // layers get enough workgroups in flight to hide the load latency
+  // ~1024 workgroups (4 waves each; set_tune key 18), at least 256 pixels (4 chunks per
+  // wave) each: small layers get enough workgroups in flight to hide the load latency
   // (512 / 256 measured 0.5 / 1.2 % slower in the step)
-  int64_t want = ceil_div(1024, tiles);
+  int64_t want = ceil_div(g_wgrad_wgs, tiles);
   int64_t maxs = ceil_div(P, 256);
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;
@@ -3039,6 +3040,18 @@ int vae2_conv2d_set_tune(int key, int value) {
   if (key == 9) {  // dconv_stream.hip: streaming direct 3x3 for 18 / 36 channels
     const int prev = g_dconv_stream;
     g_dconv_stream = value >= 0 && value <= 3 ? value : 3;
+    return prev;
+  }
+  if (key == 18) {  // gather weight gradient: target workgroups (split count)
+    if (value < 256 || value > 8192) return -1;
+    const int prev = g_wgrad_wgs;
+    g_wgrad_wgs = value;
+    return prev;
+  }
+  if (key == 19) {  // bn.hip: BatchNorm blocks per layer (at most)
+    if (value < 256 || value > 8192) return -1;
+    const int prev = g_bn_blocks;
+    g_bn_blocks = value;
     return prev;
   }
   if (key == 16) {  // wgrad_narrow.hip: minimum tiles per split (partial slab)
