@@ -73,7 +73,7 @@ constexpr int kDsLW = 34;    // halo columns of a 32-column strip
 
 // (exported symbol: the launch log names kernels through the dynamic symbol table)
 template <int TN, int NR, int Q, bool FLIP, int BNX, bool BL>
-__global__ __launch_bounds__(256) void dconv3s_kernel(DStream p) {
+__global__ __launch_bounds__(256, Q == 5 ? 4 : 1) void dconv3s_kernel(DStream p) {
   constexpr int TM = 2, LW = kDsLW, RING = kDsRing;
   constexpr int CSP = 4 * Q + 4;               // LDS floats per pixel (+4: bank spread)
   constexpr int RS = LW * CSP;                 // LDS floats per ring row
