@@ -41,13 +41,19 @@ def main():
     ap.add_argument("--res", type=int, default=1)
     ap.add_argument("--tune", default="", help="vae2_conv2d_set_tune key=value[,key=value]")
     ap.add_argument("--mask", type=int, default=0, help="ReLU mask bytes (residual layers)")
+    ap.add_argument("--set", default="level", choices=["level", "narrow", "wide"],
+                    help="level: 18/36/72/144 at 1, 1/2, 1/4, 1/8 of 128x256; narrow: the "
+                         "18/36/72 launch; wide: one 64-channel layer at 128x256")
+    ap.add_argument("--only", default="", help="comma list of passes (apply,bwd_reduce,bwd_apply)")
     a = ap.parse_args()
     lib = _lib.load()
     for kv in filter(None, a.tune.split(",")):
         k, v = kv.split("=")
         lib.vae2_conv2d_set_tune(int(k), int(v))
     dev = torch.device("cuda")
-    shapes = [(128, 256, 18), (64, 128, 36), (32, 64, 72), (16, 32, 144)]
+    shapes = {"level": [(128, 256, 18), (64, 128, 36), (32, 64, 72), (16, 32, 144)],
+              "narrow": [(128, 256, 18), (64, 128, 36), (32, 64, 72)],
+              "wide": [(128, 256, 64)]}[a.set]
     lay = (_lib.BnLayer * len(shapes))()
     keep = []
     nbytes = {"apply": 0, "bwd_reduce": 0, "bwd_apply": 0}
@@ -75,6 +81,8 @@ def main():
     for name, fn in (("apply", lambda: call("vae2_bn_multi_apply", n, lay, s)),
                      ("bwd_reduce", lambda: call("vae2_bn_multi_bwd_reduce", n, lay, s)),
                      ("bwd_apply", lambda: call("vae2_bn_multi_bwd_apply", n, lay, s))):
+        if a.only and name not in a.only.split(","):
+            continue
         us = timeit(fn, a.iters)
         print(f"  {name:12s} {us:8.1f} us  {nbytes[name] / us / 1e3:8.1f} GB/s")
 
