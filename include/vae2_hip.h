@@ -86,8 +86,10 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * key 16 = the narrow 3x3 weight gradient's minimum tiles per partial slab (1..2, default 2);
  * key 17 = the streaming 3x3's minimum 4-row steps per band (1..2, default 1); key 18 = the
  * gather weight gradient's target workgroups (256..8192, default 1024); key 19 = BatchNorm
- * blocks per layer at most (256..8192, default 1024).  Returns the previous value, -1 for an unknown key or an
- * out-of-range value of keys 4, 6, 7 and 16-19 (the setting is then left unchanged).    */
+ * blocks per layer at most (256..8192, default 1024); key 20 = the multi-layer BatchNorm
+ * apply kernels' resident-block budget (0 = one workgroup per pixel chunk, the default; R > 0:
+ * ceil(T / ceil(T / R)) workgroups stride over the T chunks).  Returns the previous value, -1 for an unknown key or an
+ * out-of-range value of keys 4, 6, 7 and 16-20 (the setting is then left unchanged).    */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab

@@ -24,6 +24,11 @@ namespace vae2 {
 static inline int quad_rows(int64_t C);
 constexpr int kPassU = 4;  // = kApplyU (defined with the apply kernels below)
 int g_bn_blocks = 1024;  // vae2_conv2d_set_tune key 19: blocks per layer (at most, whole passes)
+// vae2_conv2d_set_tune key 20: the multi-layer apply kernels' resident-block budget R (0 =
+// one workgroup per pixel chunk): a launch of T chunks runs ceil(T / ceil(T / R)) workgroups
+// striding over them, so every workgroup does the same number of chunks in one round instead
+// of a partial last round of blocks (the 18 / 36 / 72-channel launch: 2,165 chunks)
+int g_bn_apply_res = 0;
 
 static int64_t pix_per_block(int64_t P, int64_t C) {
   const int64_t pass = (int64_t)quad_rows(C) * kPassU;
@@ -611,6 +616,7 @@ struct BnMulti {
   BnLayer L[kBnMaxLayers];
   int n;
   int v2;  // buffer-resource bodies (every extent < 2 GB; vae2_conv2d_set_tune key 8)
+  int total;  // pixel chunks of the launch (apply kernels: workgroups stride over them)
 };
 
 // vae2_conv2d_set_tune key 8: 0 = the round-4 pointer-arithmetic BatchNorm bodies (A/B)
@@ -741,8 +747,10 @@ __device__ __forceinline__ void bn_apply_body2(const BnLayer& L, int blk) {
 }
 
 __global__ __launch_bounds__(256) void bn_apply_multi_kernel(BnMulti m) {
-  const int i = bn_layer_of(m, blockIdx.x);
-  bn_apply_body2(m.L[i], blockIdx.x - m.L[i].blk0);
+  for (int b = blockIdx.x; b < m.total; b += gridDim.x) {  // (once unless key 20 is set)
+    const int i = bn_layer_of(m, b);
+    bn_apply_body2(m.L[i], b - m.L[i].blk0);
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_apply_multi_r4_kernel(BnMulti m) {
@@ -1224,8 +1232,10 @@ __device__ __forceinline__ void bn_bwd_apply_body2(const BnLayer& L, int blk) {
 
 template <int ACT, bool RB, bool DACC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_multi_kernel(BnMulti m) {
-  const int i = bn_layer_of(m, blockIdx.x);
-  bn_bwd_apply_body2<ACT, RB, DACC>(m.L[i], blockIdx.x - m.L[i].blk0);
+  for (int b = blockIdx.x; b < m.total; b += gridDim.x) {  // (once unless key 20 is set)
+    const int i = bn_layer_of(m, b);
+    bn_bwd_apply_body2<ACT, RB, DACC>(m.L[i], b - m.L[i].blk0);
+  }
 }
 
 // The specialisation of a launch: the union of its layers' features.
@@ -1649,6 +1659,7 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
     }
     if (blocks == 0) continue;
     m.v2 = g_bn_v2;
+    m.total = blocks;
     for (int j = 0; j < m.n; ++j) {  // 32-bit buffer offsets: every extent below 2 GB
       const vae2_bn_layer& l = ls[i0 + j];
       const int64_t P = act_pixels(&l.xd);
@@ -1657,6 +1668,10 @@ static int bn_multi_launch(int n, const vae2_bn_layer* ls, int kind, void* strea
       if (ext >= (int64_t(1) << 31)) m.v2 = 0;
     }
     hipStream_t st = as_stream(stream);
+    if (kind != 1 && m.v2 && g_bn_apply_res > 0 && blocks > g_bn_apply_res) {
+      const int rounds = (blocks + g_bn_apply_res - 1) / g_bn_apply_res;
+      blocks = (blocks + rounds - 1) / rounds;  // (m.total keeps the chunk count)
+    }
     if (kind == 0 && m.v2)
       VAE2_LAUNCH(bn_apply_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, m);
     else if (kind == 0)

@@ -3048,6 +3048,12 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_wgrad_wgs = value;
     return prev;
   }
+  if (key == 20) {  // bn.hip: apply kernels' resident-block budget (0 = one block per chunk)
+    if (value < 0 || value > 65536) return -1;
+    const int prev = g_bn_apply_res;
+    g_bn_apply_res = value;
+    return prev;
+  }
   if (key == 19) {  // bn.hip: BatchNorm blocks per layer (at most)
     if (value < 256 || value > 8192) return -1;
     const int prev = g_bn_blocks;
