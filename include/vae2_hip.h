@@ -82,14 +82,15 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * convs with 18 / 36 output channels as 16 + 2 / 32 + 4 (VALU remainder columns); keys
  * 7-13: see vae2_conv2d_set_tune in csrc/conv.hip; key 14 = 1: the 72-channel direct 3x3
  * as two N blocks of 32 + 4 (off: measured slower); key 15 = 1 (default): direct 3x3
- * layers whose 4-row tiles leave <= 2 workgroups per CU split K over 8-wave workgroups;
+ * layers whose 4-row tiles leave <= 2 workgroups per CU split K over 8-wave workgroups
+ * (2 = over 16-wave workgroups, 4 shares; 0 = off);
  * key 16 = the narrow 3x3 weight gradient's minimum tiles per partial slab (1..2, default 2);
  * key 17 = the streaming 3x3's minimum 4-row steps per band (1..2, default 1); key 18 = the
  * gather weight gradient's target workgroups (256..8192, default 1024); key 19 = BatchNorm
  * blocks per layer at most (256..8192, default 1024); key 20 = the multi-layer BatchNorm
  * apply kernels' resident-block budget (0 = one workgroup per pixel chunk, the default; R > 0:
  * ceil(T / ceil(T / R)) workgroups stride over the T chunks).  Returns the previous value, -1 for an unknown key or an
- * out-of-range value of keys 4, 6, 7 and 16-20 (the setting is then left unchanged).    */
+ * out-of-range value of keys 4, 6, 7 and 15-20 (the setting is then left unchanged).    */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every
  * vae2_conv2d_bwd_weight(_ld) launches its partial-slab kernel and queues the slab

@@ -2,8 +2,9 @@
 branch at 32 x 64: 256 workgroups, one wave per SIMD; enc_hrnet.py:27-62):
   split72 (vae2_conv2d_set_tune key 14): 72 channels as two N blocks of 32 MFMA + 4 VALU
           channels instead of two padded 48-column blocks;
-  ksp     (key 15): the same 4-row tiles as 8-wave workgroups splitting K in two (K chunk
-          pairs alternate between the wave sets, summed through LDS in a fixed order).
+  ksp     (key 15 = 1): the same 4-row tiles as 8-wave workgroups splitting K in two (K chunk
+          pairs alternate between the wave sets, summed through LDS in a fixed order);
+  ksp4    (key 15 = 2): 16-wave workgroups, K in four shares.
 Each against fp64 PyTorch and against the default form: forward (+ bias, + beta * y, BN
 partial statistics), forward with the producer BatchNorm applied in the staging, data
 gradient (+ beta) and the data gradient's producer-BatchNorm backward partials.  Shapes: the
@@ -28,7 +29,7 @@ SHAPES = [
     (8, 32, 128, 64, 64),  # ksp only: one N block of 4 tiles
     (8, 32, 128, 32, 32),  # ksp only: 2 tiles
 ]
-KEY = {"split72": 14, "ksp": 15}
+KEY = {"split72": (14, 1), "ksp": (15, 1), "ksp4": (15, 2)}
 
 
 def _lib():
@@ -36,12 +37,12 @@ def _lib():
     return _lib.load()
 
 
-@pytest.fixture(params=["split72", "ksp"])
+@pytest.fixture(params=["split72", "ksp", "ksp4"])
 def form(request):
     lib = _lib()
     prev = lib.vae2_conv2d_set_algo(0)
-    prevs = {k: lib.vae2_conv2d_set_tune(k, 0) for k in KEY.values()}
-    lib.vae2_conv2d_set_tune(KEY[request.param], 1)
+    prevs = {k: lib.vae2_conv2d_set_tune(k, 0) for k in (14, 15)}
+    lib.vae2_conv2d_set_tune(*KEY[request.param])
     yield request.param
     for k, v in prevs.items():
         lib.vae2_conv2d_set_tune(k, v)
@@ -49,7 +50,8 @@ def form(request):
 
 
 def _switch(form, on):
-    _lib().vae2_conv2d_set_tune(KEY[form], 1 if on else 0)
+    key, val = KEY[form]
+    _lib().vae2_conv2d_set_tune(key, val if on else 0)
 
 
 def _skip(form, shape):
@@ -72,7 +74,8 @@ def _check(form, names, flip, on=True):
     if form == "split72":
         assert (int(a[1]), int(a[4])) == ((2, 4) if on else (3, 0)), a
     else:
-        assert (a[6:8] == ["8", "true"]) == on and int(a[4]) == 0, a
+        ks = (2 if form == "ksp" else 4) if on else 1
+        assert a[6:8] == [str(4 * ks), str(ks)] and int(a[4]) == 0, a
 
 
 @pytest.mark.parametrize("shape", SHAPES)

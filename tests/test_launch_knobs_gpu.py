@@ -25,6 +25,7 @@ KNOBS = [
     (17, 2, False),      # streaming 3x3: at least 2 steps per band
     (0, 0, False),       # gather GEMM: the 4-row-tile rule alone
     (15, 0, False),      # direct 3x3: no K split over 8 waves
+    (15, 2, False),      # ... or over 16 waves (4 K shares)
 ]
 
 
@@ -83,7 +84,8 @@ def test_knob_range_checks():
     """Out-of-range values are rejected (-1) and leave the setting unchanged."""
     from vae2 import _lib
     lib = _lib.load()
-    for key, bad in [(16, 0), (16, 3), (17, 0), (17, 3), (18, 100), (19, 100000), (20, -1)]:
-        before = lib.vae2_conv2d_set_tune(key, {16: 2, 17: 1, 18: 1024, 19: 1024, 20: 0}[key])
+    for key, bad in [(15, 3), (16, 0), (16, 3), (17, 0), (17, 3), (18, 100), (19, 100000),
+                     (20, -1)]:
+        before = lib.vae2_conv2d_set_tune(key, {15: 1, 16: 2, 17: 1, 18: 1024, 19: 1024, 20: 0}[key])
         assert lib.vae2_conv2d_set_tune(key, bad) == -1, (key, bad)
         lib.vae2_conv2d_set_tune(key, before)

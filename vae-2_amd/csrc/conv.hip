@@ -945,7 +945,7 @@ constexpr int kDcMaxCs4 = 8;  // quads per slab
 // (A offset, weight offset) of every K step of a slab (chunks of 4 (tap, quad) steps, an
 // even number of chunks, + the 2 chunks the loop prefetches past the end), in LDS after
 // the tile and the remainder weights
-constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 16;
+constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 32;  // (+ 8 KS, KS <= 4)
 
 // One output tile: bm = tile index (image-major), by = N block, nrows = tiles of the
 // layer (rows of its BN partial statistics).
@@ -962,31 +962,31 @@ constexpr int kDcTab = ((9 * kDcMaxCs4 + 7) / 8) * 8 + 16;
 // epilogue (DConv::bx, data gradient).
 // NW = waves per workgroup (4, or 8 with TM = 2: the same 8-row tile as TM = 4, each wave
 // owning one row -- twice the waves per SIMD for the same LDS tile)
-// KSP (NW = 8, NR = 0, fp32 operands): the 4 row waves' tile of the NW = 4 form with the K
-// chunk pairs split between two wave sets (set 0: pairs 0, 2, 4, ..., set 1: 1, 3, 5, ...),
-// set 1's accumulators added to set 0's through LDS in a fixed order before the epilogue --
-// two waves per SIMD for layers whose tiles give one workgroup per CU (set_tune key 15)
+// KS > 1 (NW = 4 KS, NR = 0, fp32 operands): the 4 row waves' tile of the NW = 4 form with
+// the K chunk pairs split between KS wave sets (set s: pairs s, s + KS, s + 2 KS, ...), sets
+// 1 .. KS-1's accumulators added to set 0's through LDS in a fixed order before the epilogue
+// -- KS waves per SIMD for layers whose tiles give one workgroup per CU (set_tune key 15)
 template <int TM, int TN, bool FLIP, bool BF, int NR = 0, int BNX = 0, int NW = 4,
-          bool KSP = false>
+          int KS = 1>
 __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const int by,
                                             const int nrows, float* __restrict__ tile) {
   constexpr int NT = 64 * NW;
-  constexpr int NWR = KSP ? NW / 2 : NW;  // waves per K share: the tile's row waves
-  static_assert(!KSP || (NW == 8 && NR == 0 && !BF), "K split form");
+  constexpr int NWR = NW / KS;  // waves per K share: the tile's row waves
+  static_assert(KS == 1 || (NW == 4 * KS && NR == 0 && !BF), "K split form");
   constexpr int BH = NWR * TM / 2, LH = BH + 2, LW = kDcBW + 2;
   constexpr int BN = 16 * TN;
   constexpr int BNT = BN + NR;             // channels of this block (MFMA + VALU)
   static_assert(NR == 0 || (!BF && NR <= 8), "remainder shape");
   __shared__ float red[NW][2][BNT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = KSP ? wave % NWR : wave, kp = KSP ? wave / NWR : 0;  // row wave, K share
+  const int wr = wave % NWR, kp = wave / NWR;  // row wave, K share
   const int g = lane >> 4, r = lane & 15;
   const int per_img = p.tiles_h * p.tiles_w;
   const int img = bm / per_img;
   const int trem = bm - img * per_img;
   const int th = trem / p.tiles_w;
   const int oh0 = th * BH, ow0 = (trem - th * p.tiles_w) * kDcBW;
-  // first output row of this wave (K share 1 of the KSP form: past the image, so its
+  // first output row of this wave (K shares > 0 of the KS form: past the image, so their
   // epilogue stores, loads and statistics are all masked off)
   const int ohw = kp ? (1 << 24) : oh0 + wr * (TM / 2);
   const int n0 = by * BNT;  // (NR > 0 with two N blocks: 72 = 2 x (32 + 4), set_tune key 14)
@@ -1044,8 +1044,9 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     const int nch = (9 * qs + 3) >> 2;
     {  // the slab's K-step table: entry k = (tap, quad) step k of the chunk sequence
       const int k = threadIdx.x;
-      // (steps past the 9 taps: zero weights; KSP prefetches up to 2 chunks further)
-      if (k < ((nch + 1) >> 1) * 8 + (KSP ? 16 : 8)) {
+      // (steps past the 9 taps: zero weights; the KS form prefetches up to 2 (KS - 1)
+      //  chunks further)
+      if (k < ((nch + 1) >> 1) * 8 + 8 * KS) {
         const int t = k / qs, q = k - t * qs;
         const bool tv = t < 9;
         const int tt = tv ? t : 0;
@@ -1123,7 +1124,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     __syncthreads();
     // ---- 9 taps x qs quads of K from LDS ----
     // chunk c, lane group g: K step 4c + g, its A / weight offsets from the table
-    int kc = g + 8 * kp;  // (KSP share 1 starts at chunk pair 1)
+    int kc = g + 8 * kp;  // (K share kp starts at chunk pair kp)
     auto load = [&](f4* fa, f4* fb) {
       const int2 e = tab[kc];
       kc += 4;
@@ -1154,9 +1155,9 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     };
     if (!BF) {
       load(fa0, fb0);
-      for (int ch = 2 * kp; ch < ((VAE2_ABLATE & 4) ? 0 : nch); ch += KSP ? 4 : 2) {
+      for (int ch = 2 * kp; ch < ((VAE2_ABLATE & 4) ? 0 : nch); ch += 2 * KS) {
         load(fa1, fb1);
-        if (KSP) kc += 8;  // (the other share's pair)
+        if (KS > 1) kc += 8 * (KS - 1);  // (the other shares' pairs)
         mma(fa0, fb0);
         rem(fa0);
         load(fa0, fb0);
@@ -1183,21 +1184,25 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
     }
   }
 
-  if constexpr (KSP) {  // K share 1's accumulators onto share 0's (fixed order)
+  if constexpr (KS > 1) {  // K shares 1 .. KS-1's accumulators onto share 0's (fixed order)
     __syncthreads();  // every wave's last reads of the tile are done
-    f4* const kred = reinterpret_cast<f4*>(tile);  // [NWR][TM][TN][64]
+    f4* const kred = reinterpret_cast<f4*>(tile);  // [KS - 1][NWR][TM][TN][64]
     if (kp) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) kred[((wr * TM + i) * TN + j) * 64 + lane] = acc[i][j];
+        for (int j = 0; j < TN; ++j)
+          kred[((((kp - 1) * NWR + wr) * TM + i) * TN + j) * 64 + lane] = acc[i][j];
     }
     __syncthreads();
     if (!kp) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int sh = 0; sh < KS - 1; ++sh)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] += kred[((wr * TM + i) * TN + j) * 64 + lane];
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] += kred[(((sh * NWR + wr) * TM + i) * TN + j) * 64 + lane];
     }
   }
 
@@ -1455,12 +1460,12 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
 }
 
 template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0, int BNX = 0, int NW = 4,
-          bool KSP = false>
+          int KS = 1>
 __global__ __launch_bounds__(64 * NW) void dconv3_kernel(DConv p) {
   static_assert(BNX == 0 || (!BF && (BNX == 1) != FLIP), "input BN: forward; partials: dgrad");
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  dconv3_body<TM, TN, FLIP, BF, NR, BNX, NW, KSP>(p, xcd_remap(blockIdx.x, gridDim.x),
-                                                  blockIdx.y, gridDim.x, tile);
+  dconv3_body<TM, TN, FLIP, BF, NR, BNX, NW, KS>(p, xcd_remap(blockIdx.x, gridDim.x),
+                                                 blockIdx.y, gridDim.x, tile);
 }
 
 // Up to kDcGroup independent layers with the same tile shape in one launch (the lock-
@@ -1535,7 +1540,7 @@ int g_wgrad_narrow = 3;   // vae2_conv2d_set_tune key 7: wgrad_narrow.hip for 18
 int g_igemm_tab = 1;      // vae2_conv2d_set_tune key 12: the gather GEMM's K-step table
 int g_dconv_n16 = 0;      // vae2_conv2d_set_tune key 13: direct 3x3 16-channel N blocks when short of workgroups
 int g_dconv_split72 = 0;  // vae2_conv2d_set_tune key 14: 72-channel direct 3x3 as two 32 + 4 N blocks
-int g_dconv_ksp = 1;      // vae2_conv2d_set_tune key 15: direct 3x3 K split over 8 waves when short of workgroups
+int g_dconv_ksp = 1;      // vae2_conv2d_set_tune key 15: direct 3x3 K split when short of workgroups (0 off, 1: 2 shares / 8 waves, 2: 4 shares / 16 waves)
 int g_wgrad_wgs = 1024;   // vae2_conv2d_set_tune key 18: gather weight-gradient target workgroups
 extern int g_bn_v2;       // bn.hip; vae2_conv2d_set_tune key 8
 #else
@@ -2504,7 +2509,7 @@ struct DTile {
   int tm, tn, nblk, cs4, tiles_h, tiles_w;
   int nr = 0;  // output channels on the VALU beside the MFMA tiles (dconv3_body NR)
   int nw = 4;  // waves per workgroup (dconv3_body NW); tile rows = nw * tm / 2
-  bool ksp = false;  // K split over 2 x 4 waves (dconv3_body KSP, nw = 8, tile rows = 2 tm)
+  int ks = 1;  // K shares over 4-wave sets (dconv3_body KS, nw = 4 ks, tile rows = 2 tm)
 };
 
 
@@ -2578,8 +2583,8 @@ static DTile pick_dtile(const vae2_act* ad, const vae2_act* yd, bool remainder =
   // frames/s over 2 A/B pairs, scripts/gpu_r6_n.sh)
   if (g_dconv_ksp && !g_bf16 && d.nr == 0 && d.tm == 2 && d.nw == 4 && d.tn >= 2 &&
       ad->n * d.tiles_h * d.tiles_w * d.nblk < 512) {
-    d.ksp = true;
-    d.nw = 8;
+    d.ks = g_dconv_ksp == 2 ? 4 : 2;
+    d.nw = 4 * d.ks;
   }
   return d;
 }
@@ -2655,16 +2660,16 @@ static void dconv_launch_tn(const DConv& p, int tn, dim3 grid, size_t shm, hipSt
   }
 }
 
-// KSP form (pick_dtile, set_tune key 15): TM = 2, 8 waves, fp32 operands, no remainder
-template <bool FLIP>
+// K-split form (pick_dtile, set_tune key 15): TM = 2, 4 KS waves, fp32 operands, no remainder
+template <bool FLIP, int KS>
 static void dconv_launch_ksp(const DConv& p, int tn, dim3 grid, size_t shm, hipStream_t s) {
-  constexpr int X = FLIP ? 2 : 1;
+  constexpr int X = FLIP ? 2 : 1, NW = 4 * KS;
   const bool bn = p.isave || p.bx;
   switch (tn) {
-#define CASE(T)                                                                                   \
-  case T:                                                                                         \
-    if (bn) VAE2_LAUNCH((dconv3_kernel<2, T, FLIP, false, 0, X, 8, true>), grid, dim3(512), shm, s, p); \
-    else VAE2_LAUNCH((dconv3_kernel<2, T, FLIP, false, 0, 0, 8, true>), grid, dim3(512), shm, s, p);    \
+#define CASE(T)                                                                                        \
+  case T:                                                                                              \
+    if (bn) VAE2_LAUNCH((dconv3_kernel<2, T, FLIP, false, 0, X, NW, KS>), grid, dim3(64 * NW), shm, s, p); \
+    else VAE2_LAUNCH((dconv3_kernel<2, T, FLIP, false, 0, 0, NW, KS>), grid, dim3(64 * NW), shm, s, p);    \
     break;
     CASE(2) CASE(3) CASE(4)
 #undef CASE
@@ -2688,11 +2693,12 @@ static DConv make_dconv(const DTile& d, const float* a, const vae2_act* ad, cons
 }
 
 static size_t dconv_shm(const DTile& d) {
-  const int rows = (d.ksp ? 4 : d.nw) * d.tm / 2;  // output rows of a tile (KSP: 4 row waves)
+  const int rows = (d.ks > 1 ? 4 : d.nw) * d.tm / 2;  // output rows of a tile (KS: 4 row waves)
   const size_t stage = ((size_t)(rows + 2) * (kDcBW + 2) * (d.cs4 * 4 + 4) +
                         (size_t)d.nr * ((9 * d.cs4 + 7) / 8) * 32 + 2 * kDcTab) * sizeof(float);
-  // KSP: share 1's accumulators ([4 waves][TM][TN][64] f4) in the same LDS after the K loop
-  const size_t kred = d.ksp ? (size_t)4 * d.tm * d.tn * 64 * 16 : 0;
+  // KS > 1: shares 1 .. KS-1's accumulators ([KS - 1][4 waves][TM][TN][64] f4) in the same
+  // LDS after the K loop
+  const size_t kred = (size_t)(d.ks - 1) * 4 * d.tm * d.tn * 64 * 16;
   return stage > kred ? stage : kred;
 }
 
@@ -2733,9 +2739,12 @@ int launch_dconv(const float* a, const vae2_act* ad, const float* wp, uint32_t w
   p.vec_out = g_vec_out && vec_ok(y, (int)yd->ps) && !(stats && beta != 0.f);
   dim3 grid((unsigned)(ad->n * d.tiles_h * d.tiles_w), (unsigned)d.nblk);
   const size_t shm = dconv_shm(d);
-  if (d.ksp) {
-    if (flip) dconv_launch_ksp<true>(p, d.tn, grid, shm, s);
-    else dconv_launch_ksp<false>(p, d.tn, grid, shm, s);
+  if (d.ks == 4) {
+    if (flip) dconv_launch_ksp<true, 4>(p, d.tn, grid, shm, s);
+    else dconv_launch_ksp<false, 4>(p, d.tn, grid, shm, s);
+  } else if (d.ks == 2) {
+    if (flip) dconv_launch_ksp<true, 2>(p, d.tn, grid, shm, s);
+    else dconv_launch_ksp<false, 2>(p, d.tn, grid, shm, s);
   } else if (d.nw == 8) {
     if (flip) dconv_launch_tn<2, true, 8>(p, d.tn, grid, shm, s, d.nr);
     else dconv_launch_tn<2, false, 8>(p, d.tn, grid, shm, s, d.nr);
@@ -3072,9 +3081,10 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_dconv_stream_spb = value;
     return prev;
   }
-  if (key == 15) {  // direct 3x3: K split over 8 waves for layers short of workgroups
+  if (key == 15) {  // direct 3x3: K split for layers short of workgroups (0, 1: 2, 2: 4 shares)
+    if (value < 0 || value > 2) return -1;
     const int prev = g_dconv_ksp;
-    g_dconv_ksp = value ? 1 : 0;
+    g_dconv_ksp = value;
     return prev;
   }
   if (key == 14) {  // direct 3x3: 72 channels as two 32 + 4 N blocks
