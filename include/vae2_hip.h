@@ -89,7 +89,8 @@ int vae2_conv2d_set_mfma_bf16(int on);
  * gather weight gradient's target workgroups (256..8192, default 1024); key 19 = BatchNorm
  * blocks per layer at most (256..8192, default 1024); key 20 = the multi-layer BatchNorm
  * apply kernels' resident-block budget (0 = one workgroup per pixel chunk, the default; R > 0:
- * ceil(T / ceil(T / R)) workgroups stride over the T chunks).  Returns the previous value, -1 for an unknown key or an
+ * ceil(T / ceil(T / R)) workgroups stride over the T chunks); key 21 = 0: the fuse sum +
+ * ReLU one channel per thread instead of one channel quad (default 1).  Returns the previous value, -1 for an unknown key or an
  * out-of-range value of keys 4, 6, 7 and 15-20 (the setting is then left unchanged).    */
 int vae2_conv2d_set_tune(int key, int value);
 /* Deferred weight-gradient reductions: while on (a per-thread switch), every

@@ -26,6 +26,7 @@ KNOBS = [
     (0, 0, False),       # gather GEMM: the 4-row-tile rule alone
     (15, 0, False),      # direct 3x3: no K split over 8 waves
     (15, 2, False),      # ... or over 16 waves (4 K shares)
+    (21, 0, True),       # fuse sum + ReLU a channel per thread instead of a quad
 ]
 
 

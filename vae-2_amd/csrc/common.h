@@ -232,7 +232,7 @@ int wgrad3n_launch(const float* x, const vae2_act* xd, const float* dy, const va
 // branches.  _shape: it takes this (input, output) pair; _rows: its BatchNorm partial rows
 // (workgroups); _launch: 1 when launched, 0 when the shape is not its own.
 extern int g_dconv_stream, g_dconv_stream_wpc, g_dconv_stream_bl, g_dconv_stream_spb,
-    g_wgrad_narrow_tps, g_bn_blocks, g_bn_apply_res;
+    g_wgrad_narrow_tps, g_bn_blocks, g_bn_apply_res, g_fuse_quad;
 bool dconv3s_shape(const vae2_act* ad, const vae2_act* yd);
 int64_t dconv3s_rows(const vae2_act* ad, const vae2_act* yd);
 int dconv3s_launch(const float* a, const vae2_act* ad, const float* wp, uint32_t w_bytes,

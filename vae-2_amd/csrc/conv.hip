@@ -3057,6 +3057,11 @@ int vae2_conv2d_set_tune(int key, int value) {
     g_wgrad_wgs = value;
     return prev;
   }
+  if (key == 21) {  // resample.hip: the fuse sum a channel quad per thread (1) or per channel
+    const int prev = g_fuse_quad;
+    g_fuse_quad = value ? 1 : 0;
+    return prev;
+  }
   if (key == 20) {  // bn.hip: apply kernels' resident-block budget (0 = one block per chunk)
     if (value < 0 || value > 65536) return -1;
     const int prev = g_bn_apply_res;

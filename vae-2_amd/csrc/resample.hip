@@ -383,6 +383,91 @@ __global__ __launch_bounds__(256) void fuse_sum_relu_kernel(FuseTerms t, float* 
   }
 }
 
+int g_fuse_quad = 1;  // vae2_conv2d_set_tune key 21: the quad form of the fuse sum (0: per channel)
+
+// The same sum, a channel quad per thread (every term and y 16-byte aligned with pixel
+// strides % 4 == 0): the pixel decode and the bilinear indices / weights are computed once
+// per quad instead of once per channel, 16-byte loads through buffer resources (a partial
+// quad reads its pixel's padding channels, whose sums are never stored), the stores of a
+// partial quad limited to its valid channels (y may be a channel slice of a wider buffer).
+// Per channel the arithmetic is fuse_sum_relu_kernel's, in the same order.
+__global__ __launch_bounds__(256, 3) void fuse_sum_relu_q_kernel(FuseTerms t, float* __restrict__ y,
+                                                              Act yd, FastDiv qdiv, FastDiv wdiv,
+                                                              FastDiv hdiv) {
+  const int C = (int)yd.c, c4 = (C + 3) >> 2;
+  const uint32_t P = (uint32_t)(yd.n * yd.h * yd.w);
+  const uint32_t total = P * (uint32_t)c4;
+  __amdgpu_buffer_rsrc_t xr[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    xr[k] = make_rsrc(k < t.n ? t.x[k] : nullptr,
+                      k < t.n ? (uint32_t)(t.d[k].n * t.d[k].h * t.d[k].w * t.d[k].ps * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(y, P * (uint32_t)yd.ps * 4u);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t p = qdiv.div(i);
+    const int c = 4 * (int)(i - p * (uint32_t)c4);
+    const uint32_t row = wdiv.div(p);
+    const uint32_t ox = p - row * (uint32_t)yd.w;
+    const uint32_t n = hdiv.div(row);
+    const uint32_t oy = row - n * (uint32_t)yd.h;
+    // every term's loads first, then the arithmetic (fuse_sum_relu_kernel's order)
+    f4 xv[4][4], scl[4], shf[4];
+    float wt[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= t.n) break;
+      const Act& d = t.d[k];
+      const uint32_t ps4 = (uint32_t)d.ps * 4u, cb = (uint32_t)c * 4u;
+      if (d.h == yd.h && d.w == yd.w) {
+        xv[k][0] = load4(xr[k], p * ps4 + cb);
+      } else {
+        const Lerp ly = lerp_index((int)oy, (int)d.h, (float)d.h / (float)yd.h);
+        const Lerp lx = lerp_index((int)ox, (int)d.w, (float)d.w / (float)yd.w);
+        const uint32_t base = n * (uint32_t)(d.h * d.w);
+        xv[k][0] = load4(xr[k], (base + (uint32_t)(ly.i0 * d.w + lx.i0)) * ps4 + cb);
+        xv[k][1] = load4(xr[k], (base + (uint32_t)(ly.i0 * d.w + lx.i1)) * ps4 + cb);
+        xv[k][2] = load4(xr[k], (base + (uint32_t)(ly.i1 * d.w + lx.i0)) * ps4 + cb);
+        xv[k][3] = load4(xr[k], (base + (uint32_t)(ly.i1 * d.w + lx.i1)) * ps4 + cb);
+        wt[k][0] = ly.l0; wt[k][1] = ly.l1; wt[k][2] = lx.l0; wt[k][3] = lx.l1;
+      }
+      if (const float* sv = t.sv[k]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ch = c + e < C ? c + e : C - 1;  // (clamped: the padding lanes are dropped)
+          scl[k][e] = sv[2 * C + ch];
+          shf[k][e] = sv[3 * C + ch];
+        }
+      }
+    }
+    f4 acc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k >= t.n) break;
+        const Act& d = t.d[k];
+        const bool bn = t.sv[k] != nullptr;
+        float v;
+        if (d.h == yd.h && d.w == yd.w) {
+          v = bn ? __builtin_fmaf(xv[k][0][e], scl[k][e], shf[k][e]) : xv[k][0][e];
+        } else {
+          float q[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            q[u] = bn ? __builtin_fmaf(xv[k][u][e], scl[k][e], shf[k][e]) : xv[k][u][e];
+          v = wt[k][0] * (wt[k][2] * q[0] + wt[k][3] * q[1]) +
+              wt[k][1] * (wt[k][2] * q[2] + wt[k][3] * q[3]);
+        }
+        a = (k == 0) ? v : a + v;
+      }
+      acc[e] = a < 0.f ? 0.f : a;  // NaN propagates (torch.relu)
+    }
+    store_quad(yr, (p * (uint32_t)yd.ps + (uint32_t)c) * 4u, acc, C - c < 4 ? C - c : 4);
+  }
+}
+
 __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy, Act dyd,
                                                        const float* __restrict__ y, Act yd,
                                                        float* __restrict__ g, Act gd,
@@ -784,6 +869,20 @@ static int fuse_sum_relu_impl(int n, const float* const* xs, const vae2_act* xds
   }
   int64_t total = act_elems(yd);
   VAE2_REQUIRE(total < (int64_t(1) << 31), fn, "tensor too large");
+  // the quad form: 16-byte aligned terms and output, pixel strides % 4 == 0, every extent
+  // addressable with 32-bit buffer offsets
+  bool quad = g_fuse_quad && (uintptr_t)y % 16 == 0 && yd->ps % 4 == 0 &&
+              act_pixels(yd) * yd->ps * 4 < (int64_t(1) << 32);
+  for (int k = 0; k < n && quad; ++k)
+    quad = (uintptr_t)xs[k] % 16 == 0 && xds[k].ps % 4 == 0 &&
+           act_pixels(&xds[k]) * xds[k].ps * 4 < (int64_t(1) << 32);
+  if (quad) {
+    const int64_t quads = act_pixels(yd) * ((yd->c + 3) / 4);
+    VAE2_LAUNCH(fuse_sum_relu_q_kernel, dim3(ew_blocks(quads, 256, 8192)), dim3(256), 0,
+                as_stream(stream), t, y, to_act(yd), FastDiv((uint32_t)((yd->c + 3) / 4)),
+                FastDiv((uint32_t)yd->w), FastDiv((uint32_t)yd->h));
+    return check_launch(fn);
+  }
   // (grid-striding over 8192 blocks: one element per thread measured 27 -> 33 us per
   // launch in the step trace -- the per-thread index setup is amortised over 2-3 elements)
   VAE2_LAUNCH(fuse_sum_relu_kernel, dim3(ew_blocks(total, 256, 8192)), dim3(256), 0,
