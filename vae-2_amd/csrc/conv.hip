@@ -1461,7 +1461,7 @@ __device__ __forceinline__ void dconv3_body(const DConv& p, const int bm, const 
 
 template <int TM, int TN, bool FLIP, bool BF = false, int NR = 0, int BNX = 0, int NW = 4,
           int KS = 1>
-__global__ __launch_bounds__(64 * NW) void dconv3_kernel(DConv p) {
+__global__ __launch_bounds__(64 * NW, (TM == 4 && TN == 4 && NR == 0 && NW == 4) ? 3 : 1) void dconv3_kernel(DConv p) {
   static_assert(BNX == 0 || (!BF && (BNX == 1) != FLIP), "input BN: forward; partials: dgrad");
   extern __shared__ __attribute__((aligned(16))) float tile[];
   dconv3_body<TM, TN, FLIP, BF, NR, BNX, NW, KS>(p, xcd_remap(blockIdx.x, gridDim.x),
